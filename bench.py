@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-2-124M bf16 training throughput (seq 1024) on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+launched by ``torch.distributed.run`` with one rank per GPU (RCCL over xGMI).
+W untimed warm-up optimizer steps, then exactly K timed optimizer steps
+bracketed by barrier + device synchronize; the elapsed time is the MAX over
+ranks; rank 0 prints one JSON line whose ``value`` is the whole-job token
+throughput (tokens/s summed over all GPUs).
+
+Every timed step is a complete training step: ``grad_accum`` micro-batches of
+forward + backward through the full 12-layer model, gradient all-reduce (N>1)
+and the fused AdamW update with global-norm clipping.  Data is synthetic
+(random token ids, fixed pool resident on the GPU), weights random-init.
+
+``--impl torch`` runs the same model on stock PyTorch ops (SDPA, F.layer_norm,
+fp32 master params under bf16 autocast, fused torch AdamW) -- the nanoGPT
+recipe minus torch.compile -- for a same-box comparison.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_TOK_S_PER_GPU = 1.07e5  # nanoGPT GPT-2-124M, 8xA100-40GB, derived
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--micro-batch", type=int, default=32)
+    ap.add_argument("--grad-accum", type=int, default=2)
+    ap.add_argument("--impl", choices=["native", "torch"], default="native")
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="print per-phase timings for this many extra steps (not part of the metric)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    torch.manual_seed(1337 + rank)
+
+    from orion_amd import ops
+    from orion_amd.models.gpt2 import build_gpt2
+    from orion_amd.train.engine import Trainer, OptimConfig
+
+    if args.impl == "torch":
+        ops.set_backend("torch")
+    else:
+        ops.load_ext(required=True)
+
+    model = build_gpt2(args.model, block_size=max(1024, args.seq_len)).to(dev)
+    n_params = model.num_params()
+    B, T, A = args.micro_batch, args.seq_len, args.grad_accum
+    vocab = model.config.vocab_size
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    pool = [(torch.randint(0, 50257, (B, T), device=dev, generator=g),
+             torch.randint(0, 50257, (B, T), device=dev, generator=g)) for _ in range(4)]
+
+    ocfg = OptimConfig(warmup_iters=10, lr_decay_iters=10000)
+    if args.impl == "native":
+        trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb)
+        step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
+    else:
+        ddp_model = model
+        if world > 1:
+            ddp_model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank],
+                                                                  bucket_cap_mb=args.bucket_mb)
+        opt = torch.optim.AdamW(model.parameters(), lr=ocfg.learning_rate, betas=(0.9, 0.95),
+                                weight_decay=0.1, fused=True)
+
+        def step_fn(i):
+            opt.zero_grad(set_to_none=True)
+            tot = 0.0
+            for j in range(A):
+                x, y = pool[(i * A + j) % 4]
+                ctx = ddp_model.no_sync() if (world > 1 and j < A - 1) else _null()
+                with ctx, torch.autocast("cuda", dtype=torch.bfloat16):
+                    _, loss = ddp_model(x, y)
+                (loss / A).backward()
+                tot = tot + loss.detach()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
+            return tot / A
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    loss = None
+    for i in range(args.warmup):
+        loss = step_fn(i)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step_fn(args.warmup + i)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    final_loss = float(loss)
+
+    tokens = world * B * T * A * args.steps
+    tok_s = tokens / elapsed
+    flops_tok = model.flops_per_token(T)
+    mfu = tok_s / world * flops_tok / 2.5e15
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec/GPU, GPT-2-124M bf16 seq=1024, at 1/2/4/8 MI355X",
+            "value": round(tok_s, 1),
+            "unit": "tokens/s (whole job, summed over n_gpus)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(tok_s / (BASELINE_TOK_S_PER_GPU * world), 3),
+            "baseline": "1.07e5 tokens/s per GPU (BASELINE.md, nanoGPT 8xA100 derived) x n_gpus",
+            "per_gpu": round(tok_s / world, 1),
+            "dtype": "bf16",
+            "data": "synthetic (random token ids), random-init weights",
+            "impl": args.impl,
+            "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
+            "loss": round(final_loss, 4),
+            "config": {"model": f"{args.model} ({n_params / 1e6:.1f}M params)",
+                       "global_batch": B * A * world, "micro_batch": B, "grad_accum": A,
+                       "seq_len": T, "tokens_per_step": B * T * A * world,
+                       "parallelism": f"dp{world}"},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,598 @@
+// Flash attention forward + backward for gfx950 (K1/K2 in SURVEY.md §2.11).
+//
+// bf16 in/out, fp32 accumulation, online softmax in base 2, causal or full,
+// GQA (Hq a multiple of Hkv), head dim D in {64, 128}.  Q/K/V/O are addressed
+// through (batch, token, head) element strides, so the packed (B, T, 3, H, D)
+// output of a fused QKV projection is consumed in place and O is written as
+// (B, T, H, D) -- no transposes around the kernel.
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 everywhere (A 32x16, B 16x32, C 32x32 with
+// C[row=(r&3)+8(r>>2)+4(l>>5)][col=l&31]).
+//
+// Forward (one 256-thread workgroup = 4 waves = 128 query rows, KV tiles of
+// 64 keys, double-buffered in LDS, one barrier per tile):
+//   * S^T = K Q^T ("swapped"): the query index is the MFMA column = the lane,
+//     so a lane holds 32 scores of ONE query; the row max / row sum need a
+//     single cross-half exchange (lane ^ 32) instead of a 32-lane butterfly;
+//   * the S^T accumulator, rounded to bf16, IS the B operand of
+//     O^T += V^T P^T (k order permuted inside a 16-key step; V^T is gathered
+//     with the matching permutation by ds_read_b64_tr_b16, the gfx950
+//     transposing LDS read), so P never touches LDS;
+//   * O^T also has the query on the lane: the online-softmax rescale is one
+//     per-lane scalar multiply.
+// Backward (one workgroup = 4 waves = 128 keys, 32 keys per wave, loop over
+// query tiles of 32 rows and over the Hq/Hkv query heads of the KV head):
+//   * S = Q K^T and dP = dO V^T with the KEY on the lane; K and V fragments
+//     stay in registers for the whole kernel;
+//   * dV^T += dO^T P and dK^T += Q^T dS take the S/dP accumulators directly as
+//     B operands (no LDS), accumulating in registers across all query tiles;
+//   * only dS crosses LDS (one 2 KB transposed image per wave) for
+//     dQ = dS K; the 4 waves' dQ partials are folded in LDS and added to an
+//     fp32 dQ buffer with one 256-byte float-atomic row per wave instruction.
+//
+// LDS images: 16-byte chunk c of row r lives at chunk c ^ f(r) with
+//   D=128: f = ((r&3)<<2)|((r>>2)&3)          (256-B rows)
+//   D=64 : f = ((r>>1)&1)<<2 | ((r>>3)&1)<<1 | ((r>>2)&1)   (128-B rows)
+// which makes BOTH the row reads (ds_read_b128, 16 distinct rows per lane
+// group) and the transposed reads (4 rows x 32 columns per half-wave)
+// conflict-free on the 64-bank LDS.
+#include "common.h"
+#include "attn_params.h"
+
+namespace orion {
+
+
+
+template <int D>
+ORION_DEVICE int swz(int r) {
+  if constexpr (D == 128) {
+    return ((r & 3) << 2) | ((r >> 2) & 3);
+  } else {
+    return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1) | ((r >> 2) & 1);
+  }
+}
+
+// element offset of (row, col) in a swizzled [rows][D] bf16 image
+template <int D>
+ORION_DEVICE int loff(int row, int col) {
+  return row * D + ((((col >> 3) ^ swz<D>(row))) << 3) + (col & 7);
+}
+
+ORION_DEVICE bf16x8 lds_b128(const bf16_t* base, int off) {
+  return *reinterpret_cast<const bf16x8*>(base + off);
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+ORION_DEVICE bf16x4 lds_tr(const bf16_t* base, int off) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
+  return __builtin_bit_cast(bf16x4, r);
+}
+
+ORION_DEVICE bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+ORION_DEVICE f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_mfma, a),
+                                                 __builtin_bit_cast(bf16x8_mfma, b), c, 0, 0, 0);
+}
+
+ORION_DEVICE f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// 16 fp32 accumulator registers rr = 8s..8s+7 -> one bf16 MFMA fragment
+ORION_DEVICE bf16x8 acc_to_frag(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(x[8 * s + j]);
+  return r;
+}
+
+// Transposed 8-element fragment of a swizzled [rows][D] image:
+// element j of lane (group g = lane>>4, i = lane&15) is image[row0 + 8*(j>>2) + (j&3)][col]
+// with row0 = rbase + (i>>2) supplied per lane and col = cbase + 16*(g&1) + 4*(i&3).
+template <int D>
+ORION_DEVICE bf16x8 tr_frag(const bf16_t* img, int rbase, int cbase, int lane, int rstep) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = rbase + (i >> 2);
+  const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
+  return cat8(lds_tr(img, loff<D>(row, col)), lds_tr(img, loff<D>(row + rstep, col)));
+}
+
+// ============================================================================ forward
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
+  constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int BH = p.B * p.Hq;
+  const int nqt = (p.T + BM - 1) / BM;
+  const int bh = blockIdx.x % BH;
+  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) tiles launch first
+  const int b = bh / p.Hq, hq = bh % p.Hq, hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qt * BM, qw0 = q0 + wv * 32;
+  const int off = p.Tk - p.T;  // causal: key <= query + off
+  const float c = p.scale_log2;
+
+  const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
+
+  bf16x8 qf[D / 16];
+  {
+    const int qr = min(qw0 + l32, p.T - 1);
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks)
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * p.q_st + ks * 16 + 8 * h32);
+  }
+  const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
+  const int ntiles = (kend + BN - 1) / BN;
+
+  bf16x8 kst[NST], vst[NST];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+      const long key = min(t * BN + row, p.Tk - 1);
+      kst[i] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ch * 8);
+      vst[i] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ch * 8);
+    }
+  };
+  auto swrite = [&](int buf) {
+    bf16_t* Ks = smem + buf * 2 * TILE;
+    bf16_t* Vs = Ks + TILE;
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+      const int o = loff<D>(row, ch * 8);
+      *reinterpret_cast<bf16x8*>(Ks + o) = kst[i];
+      *reinterpret_cast<bf16x8*>(Vs + o) = vst[i];
+    }
+  };
+
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) oacc[db] = zero16();
+  float m = -1e30f, lsum = 0.f;
+  const int myq = qw0 + l32;
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    const int k0 = t * BN;
+    const bf16_t* Ks = smem + (t & 1) * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+    const bool active = !CAUSAL || (k0 <= qw0 + 31 + off);
+    if (active) {
+      f32x16 s[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        s[kb] = zero16();
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks)
+          s[kb] = mfma32(lds_b128(Ks, loff<D>(kb * 32 + l32, ks * 16 + 8 * h32)), qf[ks], s[kb]);
+      }
+      const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw0 + off)) || (k0 + BN > p.Tk);
+      if (need_mask) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+            if (key >= p.Tk || (CAUSAL && key > myq + off)) s[kb][r] = -INFINITY;
+          }
+      }
+      float mx = m;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float alpha = __builtin_amdgcn_exp2f((m - mx) * c);
+      m = mx;
+      const float mc = mx * c;
+      float ps = 0.f;
+      bf16x8 pf[4];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * s2 + j], c, -mc));
+            ps += e;
+            pf[kb * 2 + s2][j] = f2bf(e);
+          }
+      lsum = lsum * alpha + ps;
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const bf16x8 a = tr_frag<D>(Vs, kk * 16 + 4 * h32, db * 32, lane, 8);
+          oacc[db] = mfma32(a, pf[kk], oacc[db]);
+        }
+    }
+    if (t + 1 < ntiles) swrite((t + 1) & 1);
+    __syncthreads();
+  }
+
+  const float lt = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (myq < p.T) {
+    bf16_t* Ob = p.o + b * p.o_sb + hq * p.o_sh + (long)myq * p.o_st;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(oacc[db][4 * g4 + j] * inv);
+        *reinterpret_cast<bf16x4*>(Ob + db * 32 + 8 * g4 + 4 * h32) = v4;
+      }
+    if (h32 == 0) p.lse[((long)b * p.Hq + hq) * p.T + myq] = m * c + __log2f(lt);
+  }
+}
+
+// ============================================================================ backward prep
+// delta[b][h][t] = sum_d dO * O ; 8 bf16 per lane, D/8 lanes per row.
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnParams p, float* delta) {
+  constexpr int TPR = D / 8;  // threads per row
+  const long row = (blockIdx.x * 256L + threadIdx.x) / TPR;
+  const int sub = threadIdx.x % TPR;
+  const long nrows = (long)p.B * p.Hq * p.T;
+  float s = 0.f;
+  long b = 0, h = 0, t = 0;
+  if (row < nrows) {
+    t = row % p.T;
+    h = (row / p.T) % p.Hq;
+    b = row / ((long)p.T * p.Hq);
+    const bf16x8 o = *reinterpret_cast<const bf16x8*>(p.o + b * p.o_sb + h * p.o_sh + t * p.o_st + sub * 8);
+    const bf16x8 d = *reinterpret_cast<const bf16x8*>(p.dout + b * p.do_sb + h * p.do_sh + t * p.do_st + sub * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += bf2f(o[j]) * bf2f(d[j]);
+  }
+#pragma unroll
+  for (int o2 = TPR / 2; o2 > 0; o2 >>= 1) s += __shfl_xor(s, o2, 64);
+  if (row < nrows && sub == 0) delta[row] = s;
+}
+
+// ============================================================================ backward
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnParams p) {
+  constexpr int BNK = 128, BMQ = 32, NCH = D / 8;
+  constexpr int KT = BNK * D;  // K image elements
+  constexpr int QT = BMQ * D;  // Q / dO tile elements
+  constexpr int NSTQ = BMQ * NCH / 256;  // 16-byte chunks per thread per Q/dO tile
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* Ks = smem;                       // [128][D]
+  bf16_t* Qs = Ks + KT;                    // [2][32][D]
+  bf16_t* Ds = Qs + 2 * QT;                // [2][32][D]  (dO)
+  bf16_t* St = Ds + 2 * QT;                // [4 waves][32 keys][32 q]
+  float* lse_s = reinterpret_cast<float*>(St + 4 * 32 * 32);  // [2][32]
+  float* del_s = lse_s + 64;                                  // [2][32]
+  float* dqr = del_s + 64;                                    // [4][32][D]
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int BHk = p.B * p.Hkv;
+  const int kt = blockIdx.x / BHk;  // small kt = most work under the causal mask: first
+  const int bh = blockIdx.x % BHk;
+  const int b = bh / p.Hkv, hk = bh % p.Hkv;
+  const int rep = p.Hq / p.Hkv;
+  const int kt0 = kt * BNK, kw0 = kt0 + wv * 32;
+  const int off = p.Tk - p.T;
+  const float c = p.scale_log2;
+
+  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
+
+  // K/V fragments of this wave's 32 keys (B operands of S and dP), kept in registers
+  bf16x8 kf[D / 16], vf[D / 16];
+  {
+    const long key = min(kw0 + l32, p.Tk - 1);
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ks * 16 + 8 * h32);
+    }
+  }
+  // K image for the dQ product (transposed reads)
+  for (int cidx = tid; cidx < BNK * NCH; cidx += 256) {
+    const int row = cidx / NCH, ch = cidx % NCH;
+    const long key = min(kt0 + row, p.Tk - 1);
+    *reinterpret_cast<bf16x8*>(Ks + loff<D>(row, ch * 8)) =
+        *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ch * 8);
+  }
+
+  f32x16 dka[D / 32], dva[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) { dka[db] = zero16(); dva[db] = zero16(); }
+
+  // first query row that can see any key of this workgroup
+  const int qlo = CAUSAL ? max(0, kt0 - off) : 0;
+  const int qi0 = qlo / BMQ;
+  const int nqi = (p.T + BMQ - 1) / BMQ;
+  const int iters_per_head = nqi - qi0;
+  const int total = iters_per_head * rep;
+
+  bf16x8 qst[NSTQ], dst[NSTQ];
+  float lse_r = 0.f, del_r = 0.f;
+  auto gload = [&](int it) {
+    const int hq = hk * rep + it / iters_per_head;
+    const int qbase = (qi0 + it % iters_per_head) * BMQ;
+    const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
+    const bf16_t* Db = p.dout + b * p.do_sb + hq * p.do_sh;
+#pragma unroll
+    for (int i = 0; i < NSTQ; ++i) {
+      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+      const long q = min(qbase + row, p.T - 1);
+      qst[i] = *reinterpret_cast<const bf16x8*>(Qb + q * p.q_st + ch * 8);
+      dst[i] = *reinterpret_cast<const bf16x8*>(Db + q * p.do_st + ch * 8);
+    }
+    if (tid < 32) {
+      const long q = min(qbase + tid, p.T - 1);
+      const long r = ((long)b * p.Hq + hq) * p.T + q;
+      lse_r = p.lse[r];
+      del_r = p.delta[r];
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NSTQ; ++i) {
+      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+      const int o = loff<D>(row, ch * 8);
+      *reinterpret_cast<bf16x8*>(Qs + buf * QT + o) = qst[i];
+      *reinterpret_cast<bf16x8*>(Ds + buf * QT + o) = dst[i];
+    }
+    if (tid < 32) {
+      lse_s[buf * 32 + tid] = lse_r;
+      del_s[buf * 32 + tid] = del_r;
+    }
+  };
+
+  bf16_t* Sw = St + wv * 32 * 32;
+  float* dqw = dqr + wv * 32 * D;
+  const int mykey = kw0 + l32;
+
+  if (total > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    const int hq = hk * rep + it / iters_per_head;
+    const int qbase = (qi0 + it % iters_per_head) * BMQ;
+    if (it + 1 < total) gload(it + 1);
+    const bf16_t* Qc = Qs + buf * QT;
+    const bf16_t* Dc = Ds + buf * QT;
+    const bool active = !CAUSAL || (qbase + BMQ - 1 + off >= kw0);
+    f32x16 dq[D / 32];
+    if (active) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const int o = loff<D>(l32, ks * 16 + 8 * h32);
+        s = mfma32(lds_b128(Qc, o), kf[ks], s);
+        dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
+      }
+      // P and dS in place (row q = (r&3)+8(r>>2)+4*h32 of this tile, column = mykey)
+      const bool need_mask = (CAUSAL && (qbase + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
+                             (qbase + BMQ > p.T);
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 L = *reinterpret_cast<const f32x4*>(lse_s + buf * 32 + 8 * g4 + 4 * h32);
+        const f32x4 Dl = *reinterpret_cast<const f32x4*>(del_s + buf * 32 + 8 * g4 + 4 * h32);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g4 + j;
+          float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c, -L[j]));
+          if (need_mask) {
+            const int q = qbase + 8 * g4 + 4 * h32 + j;
+            if (mykey >= p.Tk || q >= p.T || (CAUSAL && mykey > q + off)) pv = 0.f;
+          }
+          s[r] = pv;
+          dp[r] = pv * (dp[r] - Dl[j]) * p.scale;
+        }
+      }
+      bf16x8 pb[2], sb[2];
+      pb[0] = acc_to_frag(s, 0);
+      pb[1] = acc_to_frag(s, 1);
+      sb[0] = acc_to_frag(dp, 0);
+      sb[1] = acc_to_frag(dp, 1);
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          dva[db] = mfma32(tr_frag<D>(Dc, 16 * s2 + 4 * h32, db * 32, lane, 8), pb[s2], dva[db]);
+          dka[db] = mfma32(tr_frag<D>(Qc, 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
+        }
+      // dS^T image [key][q] (64-byte rows, unswizzled: the transposed read of 4 rows x 32
+      // columns covers all 64 banks exactly once)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(dp[4 * g4 + j]);
+        *reinterpret_cast<bf16x4*>(Sw + l32 * 32 + 8 * g4 + 4 * h32) = v4;
+      }
+      // dQ partial = dS K over this wave's 32 keys (A and B both by transposed reads)
+      {
+        const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+        for (int db = 0; db < D / 32; ++db) dq[db] = zero16();
+#pragma unroll
+        for (int s3 = 0; s3 < 2; ++s3) {
+          const int krow = 16 * s3 + 8 * h32 + (i >> 2);
+          const int qcol = 16 * (g & 1) + 4 * (i & 3);
+          const bf16x8 a = cat8(lds_tr(Sw, krow * 32 + qcol), lds_tr(Sw, (krow + 4) * 32 + qcol));
+#pragma unroll
+          for (int db = 0; db < D / 32; ++db) {
+            const bf16x8 bk = tr_frag<D>(Ks, wv * 32 + 16 * s3 + 8 * h32, db * 32, lane, 4);
+            dq[db] = mfma32(a, bk, dq[db]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) dq[db] = zero16();
+    }
+    // per-wave dQ partial -> LDS [q][d]
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = (r & 3) + 8 * (r >> 2) + 4 * h32;
+        dqw[q * D + db * 32 + l32] = dq[db][r];
+      }
+    if (it + 1 < total) swrite(buf ^ 1);
+    __syncthreads();
+    // fold the 4 waves and add to the fp32 dQ accumulator (256-byte rows per wave instr)
+    {
+      float* dqg = p.dq_acc + (((long)b * p.Hq + hq) * p.T) * D;
+#pragma unroll
+      for (int e = tid; e < BMQ * D; e += 256) {
+        const int q = e / D;
+        const float sum = dqr[e] + dqr[BMQ * D + e] + dqr[2 * BMQ * D + e] + dqr[3 * BMQ * D + e];
+        if (qbase + q < p.T) atomicAdd(dqg + (long)(qbase + q) * D + (e % D), sum);
+      }
+    }
+    __syncthreads();
+  }
+
+  // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
+  if (mykey < p.Tk) {
+    bf16_t* dKb = p.dk + b * p.dk_sb + hk * p.dk_sh + (long)mykey * p.dk_st;
+    bf16_t* dVb = p.dv + b * p.dv_sb + hk * p.dv_sh + (long)mykey * p.dv_st;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 k4, v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          k4[j] = f2bf(dka[db][4 * g4 + j]);
+          v4[j] = f2bf(dva[db][4 * g4 + j]);
+        }
+        *reinterpret_cast<bf16x4*>(dKb + db * 32 + 8 * g4 + 4 * h32) = k4;
+        *reinterpret_cast<bf16x4*>(dVb + db * 32 + 8 * g4 + 4 * h32) = v4;
+      }
+  }
+}
+
+// dq (bf16, strided) = dq_acc (fp32 [B][Hq][T][D])
+template <int D>
+__global__ __launch_bounds__(256) void attn_dq_convert_kernel(const float* __restrict__ acc,
+                                                              bf16_t* __restrict__ dq, long sb,
+                                                              long st, long sh, int B, int Hq,
+                                                              int T) {
+  const long n8 = (long)B * Hq * T * (D / 8);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const long e = i * 8;
+    const int d = e % D;
+    const long row = e / D;
+    const long t = row % T, h = (row / T) % Hq, b = row / ((long)T * Hq);
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(acc + e);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(acc + e + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[j] = f2bf(a0[j]); o[4 + j] = f2bf(a1[j]); }
+    *reinterpret_cast<bf16x8*>(dq + b * sb + h * sh + t * st + d) = o;
+  }
+}
+
+}  // namespace orion
+
+using namespace orion;
+
+extern "C++" {
+
+static size_t fwd_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
+static size_t bwd_lds(int D) {
+  return (size_t)128 * D * 2 + 4 * 32 * D * 2 + 4 * 32 * 32 * 2 + 128 * 4 + 4 * 32 * D * 4;
+}
+
+template <int D, bool CAUSAL>
+static void set_lds_attr() {
+  static bool done = false;
+  if (!done) {
+    hipFuncSetAttribute((const void*)attn_fwd_kernel<D, CAUSAL>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)fwd_lds(D));
+    hipFuncSetAttribute((const void*)attn_bwd_kernel<D, CAUSAL>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds(D));
+    done = true;
+  }
+}
+
+int orion_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {
+  const int BM = 128;
+  const int grid = ((p.T + BM - 1) / BM) * p.B * p.Hq;
+#define FWD(DD, CC)                                                                 \
+  set_lds_attr<DD, CC>();                                                           \
+  attn_fwd_kernel<DD, CC><<<grid, 256, fwd_lds(DD), st>>>(p);
+  if (D == 64) {
+    if (causal) { FWD(64, true) } else { FWD(64, false) }
+  } else if (D == 128) {
+    if (causal) { FWD(128, true) } else { FWD(128, false) }
+  } else {
+    return -1;
+  }
+#undef FWD
+  return (int)hipGetLastError();
+}
+
+int orion_attn_bwd(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
+  const long rows = (long)p.B * p.Hq * p.T;
+  const long threads = rows * (D / 8);
+  hipMemsetAsync(p.dq_acc, 0, (size_t)rows * D * sizeof(float), st);
+  const int pre_grid = (int)((threads + 255) / 256);
+  if (D == 64) attn_bwd_pre_kernel<64><<<pre_grid, 256, 0, st>>>(p, delta);
+  else if (D == 128) attn_bwd_pre_kernel<128><<<pre_grid, 256, 0, st>>>(p, delta);
+  else return -1;
+  AttnParams q = p;
+  q.delta = delta;
+  const int grid = ((p.Tk + 127) / 128) * p.B * p.Hkv;
+#define BWD(DD, CC)                                                                 \
+  set_lds_attr<DD, CC>();                                                           \
+  attn_bwd_kernel<DD, CC><<<grid, 256, bwd_lds(DD), st>>>(q);
+  if (D == 64) {
+    if (causal) { BWD(64, true) } else { BWD(64, false) }
+  } else {
+    if (causal) { BWD(128, true) } else { BWD(128, false) }
+  }
+#undef BWD
+  return (int)hipGetLastError();
+}
+
+int orion_attn_dq_convert(const float* acc, void* dq, long sb, long st_, long sh, int B, int Hq,
+                          int T, int D, hipStream_t st) {
+  const long n8 = (long)B * Hq * T * (D / 8);
+  long g = (n8 + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (D == 64)
+    attn_dq_convert_kernel<64><<<(int)g, 256, 0, st>>>(acc, (bf16_t*)dq, sb, st_, sh, B, Hq, T);
+  else if (D == 128)
+    attn_dq_convert_kernel<128><<<(int)g, 256, 0, st>>>(acc, (bf16_t*)dq, sb, st_, sh, B, Hq, T);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+}  // extern "C++"

@@ -1,0 +1,30 @@
+// Parameter block shared by csrc/attention.hip and csrc/bindings.cpp.
+#pragma once
+
+namespace orion {
+
+struct AttnParams {
+  const unsigned short* q;  // bf16 bits
+  const unsigned short* k;
+  const unsigned short* v;
+  unsigned short* o;
+  float* lse;  // [B][Hq][T], base-2 log-sum-exp of scaled scores
+  long q_sb, q_st, q_sh;
+  long k_sb, k_st, k_sh;
+  long v_sb, v_st, v_sh;
+  long o_sb, o_st, o_sh;
+  int B, T, Tk, Hq, Hkv;
+  float scale;       // softmax scale (1/sqrt(D))
+  float scale_log2;  // scale * log2(e)
+  // backward
+  const unsigned short* dout;
+  long do_sb, do_st, do_sh;
+  const float* delta;  // [B][Hq][T] = rowsum(dO * O)
+  float* dq_acc;       // [B][Hq][T][D] fp32
+  unsigned short* dk;
+  long dk_sb, dk_st, dk_sh;
+  unsigned short* dv;
+  long dv_sb, dv_st, dv_sh;
+};
+
+}  // namespace orion

@@ -1,0 +1,417 @@
+// torch.ops.orion_amd.* registrations for the gfx950 kernels in csrc/*.hip.
+//
+// The kernels themselves are compiled without any torch headers; this file is
+// the only place that sees at::Tensor.  Every op launches on the current
+// PyTorch HIP stream (so ops compose with torch streams and HIP-graph capture)
+// and allocates outputs through the PyTorch caching allocator.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <tuple>
+
+#include "attn_params.h"
+
+// launchers (csrc/*.hip)
+int orion_layernorm_fwd(const void*, const void*, const void*, void*, float*, float*, int, int,
+                        float, hipStream_t);
+int orion_layernorm_bwd_blocks(int rows);
+int orion_layernorm_bwd(const void*, const void*, const void*, const float*, const float*, void*,
+                        void*, void*, float*, int, int, hipStream_t);
+int orion_colsum_bf16(const void*, void*, float*, int, int, hipStream_t);
+int orion_bias_gelu_fwd(const void*, const void*, void*, long, int, hipStream_t);
+int orion_bias_gelu_bwd(const void*, const void*, const void*, void*, float*, int, int, hipStream_t);
+int orion_colsum_partials(const float*, void*, int, int, hipStream_t);
+int orion_swiglu_fwd(const void*, void*, long, int, hipStream_t);
+int orion_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
+int orion_scale_bf16(void*, const float*, long, hipStream_t);
+int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
+int orion_sumsq_partials();
+int orion_grad_sumsq(const void*, long, float*, float*, hipStream_t);
+int orion_adamw_flat(void*, float*, float*, float*, const void*, const uint8_t*, const float*,
+                     const float*, long, hipStream_t);
+int orion_rmsnorm_fwd(const void*, const void*, void*, float*, int, int, float, hipStream_t);
+int orion_rmsnorm_bwd_blocks(int rows);
+int orion_rmsnorm_bwd(const void*, const void*, const void*, const float*, void*, void*, float*,
+                      int, int, hipStream_t);
+int orion_rope(const void*, long, long, long, void*, const float*, const float*, int, int, int,
+               int, int, float, hipStream_t);
+int orion_attn_fwd(const orion::AttnParams&, int, bool, hipStream_t);
+int orion_attn_bwd(const orion::AttnParams&, int, bool, float*, hipStream_t);
+int orion_attn_dq_convert(const float*, void*, long, long, long, int, int, int, int, hipStream_t);
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
+
+void check_launch(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "orion_amd kernel launch failed: ", what, " (code ", rc, ")");
+}
+
+void check_bf16(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
+}
+
+// ------------------------------------------------------------------ layernorm
+std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& w,
+                                                 const c10::optional<Tensor>& b, double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "weight");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto xc = x.contiguous();
+  const int C = x.size(-1);
+  const int rows = x.numel() / C;
+  auto y = at::empty_like(xc);
+  auto opts = x.options().dtype(at::kFloat);
+  auto mean = at::empty({rows}, opts), rstd = at::empty({rows}, opts);
+  const void* bp = nullptr;
+  Tensor bc;
+  if (b.has_value() && b->defined()) {
+    check_bf16(*b, "bias");
+    bc = b->contiguous();
+    bp = bc.data_ptr();
+  }
+  check_launch(orion_layernorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), bp, y.data_ptr(),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, C,
+                                   (float)eps, cur_stream()),
+               "layernorm_fwd");
+  return {y, mean, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x,
+                                                 const Tensor& w, const Tensor& mean,
+                                                 const Tensor& rstd, bool has_bias) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto dyc = dy.contiguous(), xc = x.contiguous();
+  const int C = x.size(-1);
+  const int rows = x.numel() / C;
+  auto dx = at::empty_like(xc);
+  auto dw = at::empty({C}, w.options());
+  Tensor db = has_bias ? at::empty({C}, w.options()) : Tensor();
+  const int nb = orion_layernorm_bwd_blocks(rows);
+  auto part = at::empty({2 * (long)nb * C}, x.options().dtype(at::kFloat));
+  check_launch(orion_layernorm_bwd(dyc.data_ptr(), xc.data_ptr(), w.contiguous().data_ptr(),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
+                                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr,
+                                   part.data_ptr<float>(), rows, C, cur_stream()),
+               "layernorm_bwd");
+  return {dx, dw, db};
+}
+
+// ------------------------------------------------------------------ activations
+Tensor bias_gelu_fwd(const Tensor& x, const c10::optional<Tensor>& b) {
+  check_bf16(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto xc = x.contiguous();
+  auto y = at::empty_like(xc);
+  const int C = x.size(-1);
+  Tensor bc;
+  const void* bp = nullptr;
+  if (b.has_value() && b->defined()) {
+    check_bf16(*b, "bias");
+    bc = b->contiguous();
+    bp = bc.data_ptr();
+  }
+  check_launch(orion_bias_gelu_fwd(xc.data_ptr(), bp, y.data_ptr(), xc.numel(), C, cur_stream()),
+               "bias_gelu_fwd");
+  return y;
+}
+
+std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& x,
+                                         const c10::optional<Tensor>& b) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto dyc = dy.contiguous(), xc = x.contiguous();
+  const int C = x.size(-1);
+  const int rows = x.numel() / C;
+  auto dx = at::empty_like(xc);
+  Tensor db, bc;
+  const void* bp = nullptr;
+  float* part = nullptr;
+  Tensor partt;
+  if (b.has_value() && b->defined()) {
+    bc = b->contiguous();
+    bp = bc.data_ptr();
+    db = at::empty({C}, b->options());
+    const int nb = orion_layernorm_bwd_blocks(rows);
+    partt = at::empty({(long)nb * C}, x.options().dtype(at::kFloat));
+    part = partt.data_ptr<float>();
+  }
+  check_launch(orion_bias_gelu_bwd(dyc.data_ptr(), xc.data_ptr(), bp, dx.data_ptr(), part, rows,
+                                   C, cur_stream()),
+               "bias_gelu_bwd");
+  if (part) {
+    check_launch(orion_colsum_partials(part, db.data_ptr(), orion_layernorm_bwd_blocks(rows), C,
+                                       cur_stream()),
+                 "colsum");
+  }
+  return {dx, db};
+}
+
+Tensor colsum(const Tensor& m) {
+  check_bf16(m, "m");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(m.device());
+  auto mc = m.contiguous();
+  const int C = m.size(-1);
+  const int rows = m.numel() / C;
+  auto out = at::empty({C}, m.options());
+  auto part = at::empty({(long)orion_layernorm_bwd_blocks(rows) * C}, m.options().dtype(at::kFloat));
+  check_launch(orion_colsum_bf16(mc.data_ptr(), out.data_ptr(), part.data_ptr<float>(), rows, C,
+                                 cur_stream()),
+               "colsum");
+  return out;
+}
+
+Tensor swiglu_fwd(const Tensor& gu) {
+  check_bf16(gu, "gate_up");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  auto c = gu.contiguous();
+  const int F = gu.size(-1) / 2;
+  const long rows = gu.numel() / (2L * F);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto y = at::empty(sizes, gu.options());
+  check_launch(orion_swiglu_fwd(c.data_ptr(), y.data_ptr(), rows, F, cur_stream()), "swiglu_fwd");
+  return y;
+}
+
+Tensor swiglu_bwd(const Tensor& dy, const Tensor& gu) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  auto c = gu.contiguous(), d = dy.contiguous();
+  const int F = gu.size(-1) / 2;
+  const long rows = gu.numel() / (2L * F);
+  auto dgu = at::empty_like(c);
+  check_launch(orion_swiglu_bwd(d.data_ptr(), c.data_ptr(), dgu.data_ptr(), rows, F, cur_stream()),
+               "swiglu_bwd");
+  return dgu;
+}
+
+void scale_(Tensor x, const Tensor& s) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "scale_: x must be contiguous");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() == 1, "scale must be one fp32 element");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_launch(orion_scale_bf16(x.data_ptr(), s.data_ptr<float>(), x.numel(), cur_stream()), "scale_");
+}
+
+// ------------------------------------------------------------------ cross entropy
+// logits (N, V) bf16 contiguous -> overwritten with dlogits/n_valid; returns fp32 loss (scalar)
+Tensor xent_fwd_bwd(Tensor logits, const Tensor& targets, int64_t ignore_index) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(logits.is_contiguous() && logits.dim() == 2, "logits must be contiguous (N, V)");
+  TORCH_CHECK(targets.scalar_type() == at::kLong, "targets must be int64");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  const long N = logits.size(0);
+  const int V = logits.size(1);
+  auto t = targets.contiguous();
+  auto fopts = logits.options().dtype(at::kFloat);
+  auto losses = at::empty({N}, fopts);
+  auto inv_n = at::empty({1}, fopts);
+  auto loss = at::empty({}, fopts);
+  check_launch(orion_xent_fwd_bwd(logits.data_ptr(), t.data_ptr<int64_t>(), losses.data_ptr<float>(),
+                                  inv_n.data_ptr<float>(), loss.data_ptr<float>(), N, V,
+                                  ignore_index, cur_stream()),
+               "xent_fwd_bwd");
+  return loss;
+}
+
+// ------------------------------------------------------------------ optimizer
+void grad_sumsq(const Tensor& g, Tensor out) {
+  check_bf16(g, "grads");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(g.device());
+  auto part = at::empty({orion_sumsq_partials()}, g.options().dtype(at::kFloat));
+  check_launch(orion_grad_sumsq(g.data_ptr(), g.numel(), part.data_ptr<float>(),
+                                out.data_ptr<float>(), cur_stream()),
+               "grad_sumsq");
+}
+
+void adamw_flat(Tensor p16, Tensor master, Tensor m, Tensor v, const Tensor& grad,
+                const Tensor& decay, const Tensor& hyper, const Tensor& sumsq) {
+  check_bf16(p16, "params");
+  check_bf16(grad, "grads");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
+                  v.scalar_type() == at::kFloat, "optimizer state must be fp32");
+  TORCH_CHECK(decay.scalar_type() == at::kByte, "decay flags must be uint8");
+  const long n = p16.numel();
+  TORCH_CHECK(master.numel() == n && m.numel() == n && v.numel() == n && grad.numel() == n,
+              "arena size mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(p16.device());
+  check_launch(orion_adamw_flat(p16.data_ptr(), master.data_ptr<float>(), m.data_ptr<float>(),
+                                v.data_ptr<float>(), grad.data_ptr(), decay.data_ptr<uint8_t>(),
+                                hyper.data_ptr<float>(), sumsq.data_ptr<float>(), n, cur_stream()),
+               "adamw_flat");
+}
+
+// ------------------------------------------------------------------ rmsnorm / rope
+std::tuple<Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w, double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "weight");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto xc = x.contiguous();
+  const int C = x.size(-1);
+  const int rows = x.numel() / C;
+  auto y = at::empty_like(xc);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  check_launch(orion_rmsnorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), y.data_ptr(),
+                                 rstd.data_ptr<float>(), rows, C, (float)eps, cur_stream()),
+               "rmsnorm_fwd");
+  return {y, rstd};
+}
+
+std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w,
+                                       const Tensor& rstd) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto dyc = dy.contiguous(), xc = x.contiguous();
+  const int C = x.size(-1);
+  const int rows = x.numel() / C;
+  auto dx = at::empty_like(xc);
+  auto dw = at::empty({C}, w.options());
+  auto part = at::empty({(long)orion_rmsnorm_bwd_blocks(rows) * C}, x.options().dtype(at::kFloat));
+  check_launch(orion_rmsnorm_bwd(dyc.data_ptr(), xc.data_ptr(), w.contiguous().data_ptr(),
+                                 rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr(),
+                                 part.data_ptr<float>(), rows, C, cur_stream()),
+               "rmsnorm_bwd");
+  return {dx, dw};
+}
+
+// x: (B, T, H, D) view with unit stride on D; returns a contiguous rotated copy.
+Tensor rope(const Tensor& x, const Tensor& cosv, const Tensor& sinv, int64_t pos0, double sign) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "rope: x must be (B, T, H, D) with unit stride on D");
+  TORCH_CHECK(cosv.scalar_type() == at::kFloat && cosv.is_contiguous() && sinv.is_contiguous(),
+              "rope tables must be contiguous fp32");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const int B = x.size(0), T = x.size(1), H = x.size(2), D = x.size(3);
+  TORCH_CHECK(cosv.size(0) >= T + pos0 && cosv.size(1) == D / 2, "rope table too small");
+  auto y = at::empty({B, T, H, D}, x.options());
+  check_launch(orion_rope(x.data_ptr(), x.stride(0), x.stride(1), x.stride(2), y.data_ptr(),
+                          cosv.data_ptr<float>(), sinv.data_ptr<float>(), B, T, H, D, (int)pos0,
+                          (float)sign, cur_stream()),
+               "rope");
+  return y;
+}
+
+// ------------------------------------------------------------------ attention
+void fill_qkv(orion::AttnParams& p, const Tensor& q, const Tensor& k, const Tensor& v) {
+  p.q = (const unsigned short*)q.data_ptr();
+  p.k = (const unsigned short*)k.data_ptr();
+  p.v = (const unsigned short*)v.data_ptr();
+  p.q_sb = q.stride(0); p.q_st = q.stride(1); p.q_sh = q.stride(2);
+  p.k_sb = k.stride(0); p.k_st = k.stride(1); p.k_sh = k.stride(2);
+  p.v_sb = v.stride(0); p.v_st = v.stride(1); p.v_sh = v.stride(2);
+  p.B = q.size(0); p.T = q.size(1); p.Hq = q.size(2);
+  p.Tk = k.size(1); p.Hkv = k.size(2);
+}
+
+void check_attn_inputs(const Tensor& q, const Tensor& k, const Tensor& v) {
+  check_bf16(q, "q"); check_bf16(k, "k"); check_bf16(v, "v");
+  TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "attention inputs must be (B, T, H, D)");
+  TORCH_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1, "head dim must be contiguous");
+  const int D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "head dim must be 64 or 128, got ", D);
+  TORCH_CHECK(k.size(3) == D && v.size(3) == D && k.sizes() == v.sizes(), "k/v shape mismatch");
+  TORCH_CHECK(q.size(2) % k.size(2) == 0, "Hq must be a multiple of Hkv");
+  TORCH_CHECK(q.size(0) == k.size(0), "batch mismatch");
+  for (const Tensor* t : {&q, &k, &v})
+    TORCH_CHECK((t->stride(0) % 8 == 0) && (t->stride(1) % 8 == 0) && (t->stride(2) % 8 == 0) &&
+                    ((uintptr_t)t->data_ptr() % 16 == 0),
+                "attention inputs need 16-byte aligned rows");
+}
+
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, bool causal,
+                                    double scale) {
+  check_attn_inputs(q, k, v);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  orion::AttnParams p{};
+  fill_qkv(p, q, k, v);
+  const int D = q.size(3);
+  if (causal) TORCH_CHECK(p.Tk >= p.T, "causal attention needs Tk >= T");
+  auto o = at::empty({p.B, p.T, p.Hq, D}, q.options());
+  auto lse = at::empty({p.B, p.Hq, p.T}, q.options().dtype(at::kFloat));
+  p.o = (unsigned short*)o.data_ptr();
+  p.o_sb = o.stride(0); p.o_st = o.stride(1); p.o_sh = o.stride(2);
+  p.lse = lse.data_ptr<float>();
+  p.scale = (float)scale;
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  check_launch(orion_attn_fwd(p, D, causal, cur_stream()), "attn_fwd");
+  return {o, lse};
+}
+
+// dq/dk/dv: preallocated outputs (may be strided views of one packed buffer)
+void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
+              const Tensor& o, const Tensor& lse, bool causal, double scale, Tensor dq, Tensor dk,
+              Tensor dv) {
+  check_attn_inputs(q, k, v);
+  check_bf16(dout, "dout");
+  TORCH_CHECK(dout.stride(3) == 1 && o.stride(3) == 1, "dout/o head dim must be contiguous");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  orion::AttnParams p{};
+  fill_qkv(p, q, k, v);
+  const int D = q.size(3);
+  p.o = (unsigned short*)o.data_ptr();
+  p.o_sb = o.stride(0); p.o_st = o.stride(1); p.o_sh = o.stride(2);
+  p.lse = const_cast<float*>(lse.data_ptr<float>());
+  p.scale = (float)scale;
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.dout = (const unsigned short*)dout.data_ptr();
+  p.do_sb = dout.stride(0); p.do_st = dout.stride(1); p.do_sh = dout.stride(2);
+  auto fopts = q.options().dtype(at::kFloat);
+  auto dq_acc = at::empty({p.B, p.Hq, p.T, D}, fopts);
+  auto delta = at::empty({p.B, p.Hq, p.T}, fopts);
+  p.dq_acc = dq_acc.data_ptr<float>();
+  p.dk = (unsigned short*)dk.data_ptr();
+  p.dk_sb = dk.stride(0); p.dk_st = dk.stride(1); p.dk_sh = dk.stride(2);
+  p.dv = (unsigned short*)dv.data_ptr();
+  p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
+  check_launch(orion_attn_bwd(p, D, causal, delta.data_ptr<float>(), cur_stream()), "attn_bwd");
+  check_launch(orion_attn_dq_convert(dq_acc.data_ptr<float>(), dq.data_ptr(), dq.stride(0),
+                                     dq.stride(1), dq.stride(2), p.B, p.Hq, p.T, D, cur_stream()),
+               "attn_dq_convert");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(orion_amd, m) {
+  m.def("layernorm_fwd(Tensor x, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias) -> (Tensor, Tensor, Tensor)");
+  m.def("bias_gelu_fwd(Tensor x, Tensor? b) -> Tensor");
+  m.def("bias_gelu_bwd(Tensor dy, Tensor x, Tensor? b) -> (Tensor, Tensor)");
+  m.def("colsum(Tensor m) -> Tensor");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor dy, Tensor gu) -> Tensor");
+  m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
+  m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
+  m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
+  m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
+  m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd) -> (Tensor, Tensor)");
+  m.def("rope(Tensor x, Tensor cos, Tensor sin, int pos0, float sign) -> Tensor");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
+  m.impl("layernorm_fwd", &layernorm_fwd);
+  m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("bias_gelu_fwd", &bias_gelu_fwd);
+  m.impl("bias_gelu_bwd", &bias_gelu_bwd);
+  m.impl("colsum", &colsum);
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("scale_", &scale_);
+  m.impl("xent_fwd_bwd", &xent_fwd_bwd);
+  m.impl("grad_sumsq", &grad_sumsq);
+  m.impl("adamw_flat", &adamw_flat);
+  m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("rope", &rope);
+  m.impl("attn_fwd", &attn_fwd);
+  m.impl("attn_bwd", &attn_bwd);
+}

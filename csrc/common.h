@@ -1,0 +1,108 @@
+// Shared device helpers for the orion_amd gfx950 (CDNA4, MI355X) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * wave64 everywhere: lane = threadIdx.x & 63, reductions span 64 lanes;
+//   * bf16 tensors are moved as 8- or 16-byte vectors (Guideline 13 of the
+//     CDNA HIP guide: scalar bf16 loads cost ~2x);
+//   * all arithmetic in fp32, bf16 conversion with round-to-nearest-even that
+//     keeps NaN a NaN (plain cast -> v_cvt_pk_bf16_f32 at -O3).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define ORION_DEVICE __device__ __forceinline__
+
+namespace orion {
+
+typedef unsigned short bf16_t;  // raw bf16 bits
+
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned short bf16x4;
+typedef __attribute__((ext_vector_type(8))) unsigned short bf16x8;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_mfma;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_mfma;
+
+ORION_DEVICE float bf2f(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+
+ORION_DEVICE bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+ORION_DEVICE unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+
+template <int N>
+struct VecT;
+template <>
+struct VecT<4> { typedef bf16x4 type; };
+template <>
+struct VecT<8> { typedef bf16x8 type; };
+
+// ---------------------------------------------------------------- wave / block reductions
+ORION_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+ORION_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x = 64 * NW; `scratch` holds NW floats in LDS.
+template <int NW>
+ORION_DEVICE float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r += scratch[i];
+  __syncthreads();
+  return r;
+}
+
+template <int NW>
+ORION_DEVICE float block_max(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max(v);
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r = fmaxf(r, scratch[i]);
+  __syncthreads();
+  return r;
+}
+
+// GELU (tanh approximation) and its derivative, as in GPT-2 / nanoGPT.
+ORION_DEVICE float gelu_tanh_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+ORION_DEVICE float gelu_tanh_grad_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+
+ORION_DEVICE float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+}  // namespace orion
+
+#define HIP_LAUNCH_CHECK() (void)hipGetLastError()

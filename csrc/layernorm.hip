@@ -1,0 +1,323 @@
+// LayerNorm forward / backward for bf16 activations (K3 in SURVEY.md §2.11).
+//
+// Regime: memory bound (one read of x, one write of y; bwd reads x, dy, writes dx).
+// Design for wave64:
+//   * one wavefront per row, 4 rows per 256-thread workgroup; a lane owns the
+//     same VEC-wide column slices in every row it touches, so its slice of
+//     gamma/beta lives in registers and the backward's column sums
+//     (dgamma, dbeta) accumulate in registers with no atomics;
+//   * row statistics by 64-lane butterfly (__shfl_xor), two-pass variance in
+//     registers (the row is read from HBM once);
+//   * backward: a fixed grid of row-chunk workgroups writes fp32 partial column
+//     sums, a second tiny kernel folds them (deterministic, no float atomics).
+#include "common.h"
+
+namespace orion {
+
+template <int VEC>
+ORION_DEVICE void load_vec(const bf16_t* p, float* out) {
+  typedef typename VecT<VEC>::type V;
+  V v = *reinterpret_cast<const V*>(p);
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) out[j] = bf2f(v[j]);
+}
+
+template <int VEC>
+ORION_DEVICE void store_vec(bf16_t* p, const float* in) {
+  typedef typename VecT<VEC>::type V;
+  V v;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) v[j] = f2bf(in[j]);
+  *reinterpret_cast<V*>(p) = v;
+}
+
+template <int VEC, int ITERS>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+    bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    int rows, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16_t* xr = x + (size_t)row * C;
+  float v[ITERS][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int c = (i * 64 + lane) * VEC;
+    if (c < C) {
+      load_vec<VEC>(xr + c, v[i]);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) s += v[i][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  const float mean = wave_sum(s) * invC;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int c = (i * 64 + lane) * VEC;
+    if (c < C) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) * invC + eps);
+  bf16_t* yr = y + (size_t)row * C;
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int c = (i * 64 + lane) * VEC;
+    if (c < C) {
+      float wf[VEC], bfv[VEC], o[VEC];
+      load_vec<VEC>(w + c, wf);
+      if (b) load_vec<VEC>(b + c, bfv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = (v[i][j] - mean) * rstd * wf[j] + (b ? bfv[j] : 0.f);
+      store_vec<VEC>(yr + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Backward: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma.
+template <int VEC, int ITERS>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    bf16_t* __restrict__ dx, float* __restrict__ part_dw, float* __restrict__ part_db,
+    int rows, int C, int rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float wf[ITERS][VEC], adw[ITERS][VEC], adb[ITERS][VEC];
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int c = (i * 64 + lane) * VEC;
+    if (c < C) load_vec<VEC>(w + c, wf[i]);
+    else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) wf[i][j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { adw[i][j] = 0.f; adb[i][j] = 0.f; }
+  }
+  const float invC = 1.f / (float)C;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + wv; row < r1; row += 4) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    const bf16_t* xr = x + (size_t)row * C;
+    const bf16_t* dyr = dy + (size_t)row * C;
+    float xh[ITERS][VEC], g[ITERS][VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (c < C) {
+        float xv[VEC], dv[VEC];
+        load_vec<VEC>(xr + c, xv);
+        load_vec<VEC>(dyr + c, dv);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          xh[i][j] = (xv[j] - mean) * rstd;
+          g[i][j] = dv[j] * wf[i][j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+          adw[i][j] += dv[j] * xh[i][j];
+          adb[i][j] += dv[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) { xh[i][j] = 0.f; g[i][j] = 0.f; }
+      }
+    }
+    const float m1 = wave_sum(s1) * invC, m2 = wave_sum(s2) * invC;
+    bf16_t* dxr = dx + (size_t)row * C;
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (c < C) {
+        float o[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o[j] = rstd * (g[i][j] - m1 - xh[i][j] * m2);
+        store_vec<VEC>(dxr + c, o);
+      }
+    }
+  }
+  // fold the 4 waves' column partials through LDS, one output pass per quantity
+  if (part_dw) {
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (c < C) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) red[wv * C + c + j] = adw[i][j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256)
+      part_dw[(size_t)blockIdx.x * C + c] = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
+    __syncthreads();
+  }
+  if (part_db) {
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (c < C) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) red[wv * C + c + j] = adb[i][j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256)
+      part_db[(size_t)blockIdx.x * C + c] = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
+  }
+}
+
+// out[c] = sum_p part[p][c]  (bf16 output).  Block: 64 columns x 4 row phases.
+__global__ __launch_bounds__(256) void colsum_partials_kernel(
+    const float* __restrict__ part, bf16_t* __restrict__ out, int P, int C) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (c < C)
+    for (int p = wv; p < P; p += 4) s += part[(size_t)p * C + c];
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && c < C) out[c] = f2bf(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+}
+
+}  // namespace orion
+
+using namespace orion;
+
+static bool ln_pick(int C, int* vec, int* iters) {
+  if (C % 8 == 0) {
+    *vec = 8;
+    *iters = (C + 511) / 512;
+  } else if (C % 4 == 0) {
+    *vec = 4;
+    *iters = (C + 255) / 256;
+  } else {
+    return false;
+  }
+  return *iters <= 4;
+}
+
+int orion_ln_max_cols() { return 2048; }
+
+int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
+                        float* rstd, int rows, int C, float eps, hipStream_t st) {
+  int vec, it;
+  if (!ln_pick(C, &vec, &it)) return -1;
+  dim3 grid((rows + 3) / 4), block(256);
+  auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto B = (const bf16_t*)b;
+  auto Y = (bf16_t*)y;
+  if (vec == 8) {
+    switch (it) {
+      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+    }
+  } else {
+    switch (it) {
+      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+    }
+  }
+  return (int)hipGetLastError();
+}
+
+// Number of row-chunk workgroups the backward uses (caller sizes the partial buffers).
+int orion_layernorm_bwd_blocks(int rows) {
+  int nb = (rows + 63) / 64;  // >= 64 rows (16 per wave) per workgroup
+  return nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
+}
+
+int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
+                        const float* rstd, void* dx, void* dw, void* db, float* part, int rows,
+                        int C, hipStream_t st) {
+  int vec, it;
+  if (!ln_pick(C, &vec, &it)) return -1;
+  const int nb = orion_layernorm_bwd_blocks(rows);
+  const int rpb = (rows + nb - 1) / nb;
+  float* pdw = dw ? part : nullptr;
+  float* pdb = db ? part + (size_t)nb * C : nullptr;
+  const size_t lds = (size_t)4 * C * sizeof(float);
+  auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w;
+  auto DX = (bf16_t*)dx;
+  if (vec == 8) {
+    switch (it) {
+      case 1: ln_bwd_kernel<8, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 2: ln_bwd_kernel<8, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 3: ln_bwd_kernel<8, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 4: ln_bwd_kernel<8, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+    }
+  } else {
+    switch (it) {
+      case 1: ln_bwd_kernel<4, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 2: ln_bwd_kernel<4, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 3: ln_bwd_kernel<4, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 4: ln_bwd_kernel<4, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+    }
+  }
+  const int cb = (C + 63) / 64;
+  if (dw) colsum_partials_kernel<<<cb, 256, 0, st>>>(pdw, (bf16_t*)dw, nb, C);
+  if (db) colsum_partials_kernel<<<cb, 256, 0, st>>>(pdb, (bf16_t*)db, nb, C);
+  return (int)hipGetLastError();
+}
+
+// Column sum of a bf16 matrix [rows][C] into bf16 out[C] (bias gradients); uses the
+// same partial scheme.  part must hold orion_layernorm_bwd_blocks(rows) * C floats.
+__global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(
+    const bf16_t* __restrict__ m, float* __restrict__ part, int rows, int C, int rows_per_block) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = (blockIdx.y * 64 + lane) * 8;
+  const bool valid = c < C;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int r0 = blockIdx.x * rows_per_block, r1 = valid ? min(rows, r0 + rows_per_block) : 0;
+  for (int r = r0 + wv; r < r1; r += 4) {
+    float v[8];
+    load_vec<8>(m + (size_t)r * C + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  __shared__ float red[4][512];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wv][lane * 8 + j] = acc[j];
+  __syncthreads();
+  if (wv == 0 && valid) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = lane * 8 + j;
+      part[(size_t)blockIdx.x * C + c + j] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+    }
+  }
+}
+
+int orion_colsum_bf16(const void* m, void* out, float* part, int rows, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  const int nb = orion_layernorm_bwd_blocks(rows);
+  const int rpb = (rows + nb - 1) / nb;
+  dim3 grid(nb, (C / 8 + 63) / 64);
+  colsum_bf16_partial_kernel<<<grid, 256, 0, st>>>((const bf16_t*)m, part, rows, C, rpb);
+  colsum_partials_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, (bf16_t*)out, nb, C);
+  return (int)hipGetLastError();
+}
+
+int orion_colsum_partials(const float* part, void* out, int P, int C, hipStream_t st) {
+  colsum_partials_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, (bf16_t*)out, P, C);
+  return (int)hipGetLastError();
+}

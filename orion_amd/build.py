@@ -1,0 +1,103 @@
+"""Build the in-tree HIP extension ``orion_amd/_C.so`` with hipcc (gfx950).
+
+No hipify, no JIT cache, no setuptools magic: every ``csrc/*.hip`` kernel file
+is compiled by ``hipcc --offload-arch=gfx950`` into an object with no torch
+headers (fast, pure kernel code), ``csrc/bindings.cpp`` is compiled against
+the torch headers, and everything is linked into one shared object that
+registers ``torch.ops.orion_amd.*`` on load.  Objects are rebuilt only when a
+source or header is newer than the object.
+
+Usage: ``python -m orion_amd.build [-j N] [--force] [--verbose]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shlex
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "csrc")
+OUT = os.path.join(ROOT, "orion_amd", "_C.so")
+ARCH = os.environ.get("ORION_AMD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+
+
+def _torch_paths():
+    import torch
+    import torch.utils.cpp_extension as ce
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return ce.include_paths(), ce.library_paths(), abi
+
+
+def _newest_header():
+    hs = glob.glob(os.path.join(CSRC, "*.h"))
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(shlex.quote(c) for c in cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -> str:
+    incs, libdirs, abi = _torch_paths()
+    os.makedirs(BUILD, exist_ok=True)
+    hdr_time = _newest_header()
+    common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+              "-Wno-unused-result", "-Wno-unused-command-line-argument", f"-I{CSRC}"]
+    kern = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+            *common]
+    py_inc = sysconfig.get_paths()["include"]
+    bind = [HIPCC, *common, *[f"-I{i}" for i in incs], f"-I{py_inc}",
+            "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H"]
+    jobs_list = []
+    objs = []
+    for src in sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + [os.path.join(CSRC, "bindings.cpp")]:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        stale = force or not os.path.exists(obj) or \
+            os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_time)
+        if stale:
+            base = bind if src.endswith(".cpp") else kern
+            jobs_list.append(base + ["-c", src, "-o", obj])
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    if jobs_list:
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            futs = [ex.submit(_run, c, verbose) for c in jobs_list]
+            for f in futs:
+                f.result()
+    newest_obj = max(os.path.getmtime(o) for o in objs)
+    if force or jobs_list or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest_obj:
+        tlib = libdirs[0]
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp",
+                f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+                f"-Wl,-rpath,{tlib}"]
+        _run(link, verbose)
+        os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    out = build(a.jobs, a.force, a.verbose)
+    print(out)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,178 @@
+"""Fused-op layer: HIP/CDNA4 kernels on the GPU, plain PyTorch on the CPU.
+
+Every public function here dispatches on the device of its inputs:
+
+* CPU tensors -> :mod:`orion_amd.ops.reference` (the numerics oracle);
+* GPU tensors -> the hand-written gfx950 kernels in ``csrc/`` (loaded from the
+  in-tree ``orion_amd/_C*.so``), wrapped in ``torch.autograd.Function``s.
+
+There is deliberately no silent fallback on the GPU: if the extension is not
+built, a GPU call raises.  ``ORION_AMD_OPS=torch`` (or :func:`set_backend`)
+selects stock PyTorch GPU ops instead; it exists only so ``bench.py`` can
+measure the stock-PyTorch baseline on the same model.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import reference as ref
+from ._ext import ext_available, load_ext
+
+_BACKEND = os.environ.get("ORION_AMD_OPS", "hip")
+
+
+def set_backend(name: str):
+    global _BACKEND
+    assert name in ("hip", "torch"), name
+    _BACKEND = name
+
+
+def backend() -> str:
+    return _BACKEND
+
+
+def _gpu(t: torch.Tensor) -> str | None:
+    """Return 'hip' / 'torch' for GPU tensors, None for CPU tensors."""
+    if not t.is_cuda:
+        return None
+    if _BACKEND == "hip":
+        load_ext(required=True)
+        return "hip"
+    return "torch"
+
+
+# --------------------------------------------------------------------------- norms
+def layer_norm(x, weight, bias, eps=1e-5):
+    b = _gpu(x)
+    if b == "hip":
+        from .layernorm import layer_norm_hip
+        return layer_norm_hip(x, weight, bias, eps)
+    if b == "torch":
+        return F.layer_norm(x, (x.shape[-1],), weight.to(x.dtype),
+                            None if bias is None else bias.to(x.dtype), eps)
+    return ref.layer_norm(x, weight, bias, eps)
+
+
+def rms_norm(x, weight, eps=1e-5):
+    b = _gpu(x)
+    if b == "hip":
+        from .rmsnorm import rms_norm_hip
+        return rms_norm_hip(x, weight, eps)
+    if b == "torch":
+        xf = x.float()
+        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * weight.to(x.dtype)
+    return ref.rms_norm(x, weight, eps)
+
+
+# --------------------------------------------------------------------------- activations
+def gelu(x):
+    b = _gpu(x)
+    if b == "hip":
+        from .activations import bias_gelu_hip
+        return bias_gelu_hip(x, None)
+    if b == "torch":
+        return F.gelu(x, approximate="tanh")
+    return ref.gelu_tanh(x)
+
+
+def bias_gelu(x, bias):
+    b = _gpu(x)
+    if b == "hip":
+        from .activations import bias_gelu_hip
+        return bias_gelu_hip(x, bias)
+    if b == "torch":
+        return F.gelu(x + bias.to(x.dtype), approximate="tanh")
+    return ref.bias_gelu(x, bias)
+
+
+def swiglu(gate_up):
+    """silu(gate) * up on a packed (..., 2F) [gate | up] projection -> (..., F)."""
+    b = _gpu(gate_up)
+    if b == "hip":
+        from .activations import swiglu_hip
+        return swiglu_hip(gate_up)
+    gate, up = gate_up.chunk(2, dim=-1)
+    if b == "torch":
+        return F.silu(gate) * up
+    return ref.swiglu(gate, up)
+
+
+def add_broadcast(x, pos):
+    """x (B, T, C) + pos (T, C); kept as one op so the GPU path is one kernel."""
+    return x + pos.to(x.dtype)
+
+
+# --------------------------------------------------------------------------- rope
+def rope(x, cos, sin, pos0=0):
+    """Rotate-half RoPE of x (B, T, H, D) at positions pos0..pos0+T-1 (fp32 tables (Tmax, D/2))."""
+    b = _gpu(x)
+    if b == "hip":
+        from .rope import rope_hip
+        return rope_hip(x, cos, sin, pos0)
+    return ref.rope(x, cos[pos0:], sin[pos0:])
+
+
+# --------------------------------------------------------------------------- attention
+def attention_qkv(qkv, n_head, causal=True):
+    """Causal self-attention on a packed (B, T, 3C) projection -> (B, T, C)."""
+    b = _gpu(qkv)
+    if b == "hip":
+        from .attention import flash_attention_qkv
+        return flash_attention_qkv(qkv, n_head, causal)
+    if b == "torch":
+        B, T, C3 = qkv.shape
+        C = C3 // 3
+        q, k, v = qkv.view(B, T, 3, n_head, C // n_head).unbind(2)
+        y = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2),
+                                           v.transpose(1, 2), is_causal=causal)
+        return y.transpose(1, 2).reshape(B, T, C)
+    return ref.attention_qkv(qkv, n_head, causal)
+
+
+def attention(q, k, v, causal=True):
+    """Attention on (B, T, H, D) tensors (GQA when k/v have fewer heads)."""
+    b = _gpu(q)
+    if b == "hip":
+        from .attention import flash_attention
+        return flash_attention(q, k, v, causal)
+    if b == "torch":
+        rep = q.shape[2] // k.shape[2]
+        kk = k.repeat_interleave(rep, 2) if rep > 1 else k
+        vv = v.repeat_interleave(rep, 2) if rep > 1 else v
+        y = F.scaled_dot_product_attention(q.transpose(1, 2), kk.transpose(1, 2),
+                                           vv.transpose(1, 2), is_causal=causal)
+        return y.transpose(1, 2)
+    return ref.attention(q, k, v, causal)
+
+
+# --------------------------------------------------------------------------- loss
+def cross_entropy(logits, targets, ignore_index=-1):
+    b = _gpu(logits)
+    if b == "hip":
+        from .xent import fused_cross_entropy
+        return fused_cross_entropy(logits, targets, ignore_index)
+    if b == "torch":
+        return F.cross_entropy(logits.float(), targets, ignore_index=ignore_index)
+    return ref.cross_entropy(logits, targets, ignore_index)
+
+
+def linear_cross_entropy(x, weight, targets, ignore_index=-1):
+    """mean CE of softmax(x @ weight^T); x (N, C), weight (V, C) -- the fused LM head + loss."""
+    b = _gpu(x)
+    if b == "hip":
+        from .xent import linear_cross_entropy_hip
+        return linear_cross_entropy_hip(x, weight, targets, ignore_index)
+    logits = F.linear(x, weight.to(x.dtype))
+    if b == "torch":
+        return F.cross_entropy(logits.float(), targets, ignore_index=ignore_index)
+    return ref.cross_entropy(logits, targets, ignore_index)
+
+
+__all__ = [
+    "set_backend", "backend", "ext_available", "load_ext",
+    "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "rope",
+    "attention_qkv", "attention", "cross_entropy", "linear_cross_entropy",
+]

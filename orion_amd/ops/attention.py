@@ -1,0 +1,71 @@
+"""Flash-attention autograd wrappers over csrc/attention.hip.
+
+``flash_attention_qkv`` consumes the packed (B, T, 3C) output of a fused QKV
+projection through strided views and produces the packed gradient in one
+buffer, so there is no split/transpose/concat around the kernels.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._ext import C
+
+
+class _FlashQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, n_head, causal):
+        B, T, C3 = qkv.shape
+        Cm = C3 // 3
+        D = Cm // n_head
+        v5 = qkv.view(B, T, 3, n_head, D)
+        scale = 1.0 / math.sqrt(D)
+        o, lse = C().attn_fwd(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], bool(causal), scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.meta = (n_head, bool(causal), scale)
+        return o.view(B, T, Cm)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        n_head, causal, scale = ctx.meta
+        B, T, C3 = qkv.shape
+        D = C3 // 3 // n_head
+        v5 = qkv.view(B, T, 3, n_head, D)
+        dqkv = torch.empty_like(qkv)
+        d5 = dqkv.view(B, T, 3, n_head, D)
+        do4 = do.contiguous().view(B, T, n_head, D)
+        C().attn_bwd(do4, v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], o, lse, causal, scale,
+                     d5[:, :, 0], d5[:, :, 1], d5[:, :, 2])
+        return dqkv, None, None
+
+
+def flash_attention_qkv(qkv, n_head, causal=True):
+    return _FlashQKV.apply(qkv, n_head, causal)
+
+
+class _Flash(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal):
+        D = q.shape[-1]
+        scale = 1.0 / math.sqrt(D)
+        o, lse = C().attn_fwd(q, k, v, bool(causal), scale)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.meta = (bool(causal), scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        causal, scale = ctx.meta
+        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+        dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+        C().attn_bwd(do.contiguous(), q, k, v, o, lse, causal, scale, dq, dk, dv)
+        return dq, dk, dv, None
+
+
+def flash_attention(q, k, v, causal=True):
+    """q (B, T, Hq, D), k/v (B, Tk, Hkv, D) with unit stride on D -> (B, T, Hq, D)."""
+    return _Flash.apply(q, k, v, causal)

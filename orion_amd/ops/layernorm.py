@@ -1,0 +1,56 @@
+"""LayerNorm / RMSNorm autograd wrappers over the HIP kernels (csrc/layernorm.hip,
+csrc/rmsnorm_rope.hip).  Weights may be fp32 (eval/inference) or bf16 (arena);
+kernels always see bf16 and gradients are returned in the weight's dtype."""
+from __future__ import annotations
+
+import torch
+
+from ._ext import C
+
+
+def _bf16(t):
+    return t if t is None or t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        xb = _bf16(x)
+        y, mean, rstd = C().layernorm_fwd(xb, _bf16(w), _bf16(b), float(eps))
+        ctx.save_for_backward(xb, w, mean, rstd)
+        ctx.has_bias = b is not None
+        ctx.b_dtype = None if b is None else b.dtype
+        ctx.x_dtype = x.dtype
+        return y.view(x.shape).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = C().layernorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), mean, rstd,
+                                       ctx.has_bias)
+        dx = dx.view(xb.shape).to(ctx.x_dtype)
+        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_bias else None), None
+
+
+def layer_norm_hip(x, weight, bias, eps=1e-5):
+    return _LayerNorm.apply(x, weight, bias, eps)
+
+
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        xb = _bf16(x)
+        y, rstd = C().rmsnorm_fwd(xb, _bf16(w), float(eps))
+        ctx.save_for_backward(xb, w, rstd)
+        ctx.x_dtype = x.dtype
+        return y.view(x.shape).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, w, rstd = ctx.saved_tensors
+        dx, dw = C().rmsnorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), rstd)
+        return dx.view(xb.shape).to(ctx.x_dtype), dw.to(w.dtype), None
+
+
+def rms_norm_hip(x, weight, eps=1e-5):
+    return _RMSNorm.apply(x, weight, eps)

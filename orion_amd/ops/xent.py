@@ -1,0 +1,59 @@
+"""Fused softmax-cross-entropy wrappers over csrc/xent.hip.
+
+``linear_cross_entropy`` fuses the LM head: logits = x W^T (hipBLASLt GEMM),
+then one kernel computes the loss AND writes dlogits over the logits buffer,
+so backward is two GEMMs on the saved dlogits with the upstream gradient
+applied to the small (N, C) / (V, C) results.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import C
+
+
+class _LinearXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, targets, ignore_index):
+        logits = torch.nn.functional.linear(x, w)
+        loss = C().xent_fwd_bwd(logits, targets.contiguous(), int(ignore_index))
+        ctx.save_for_backward(x, w, logits)   # logits now hold dlogits / n_valid
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, dl = ctx.saved_tensors
+        s = g.detach().float().reshape(1).contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = dl @ w
+            C().scale_(dx, s)
+        if ctx.needs_input_grad[1]:
+            dw = dl.t() @ x
+            C().scale_(dw, s)
+        return dx, dw, None, None
+
+
+def linear_cross_entropy_hip(x, w, targets, ignore_index=-1):
+    """mean cross-entropy of softmax(x @ w^T) against targets; x (N, C), w (V, C)."""
+    return _LinearXent.apply(x, w, targets, ignore_index)
+
+
+class _Xent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, ignore_index):
+        buf = logits.detach().contiguous().clone()
+        loss = C().xent_fwd_bwd(buf, targets.contiguous(), int(ignore_index))
+        ctx.save_for_backward(buf)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        out = dl.clone()
+        C().scale_(out, g.detach().float().reshape(1).contiguous())
+        return out, None, None
+
+
+def fused_cross_entropy(logits, targets, ignore_index=-1):
+    return _Xent.apply(logits, targets, ignore_index)

@@ -1,0 +1,100 @@
+"""Flat parameter / gradient arenas.
+
+All trainable parameters of a model are re-homed into ONE contiguous bf16
+buffer (what the GEMMs read) and their gradients into ONE contiguous buffer
+(what autograd accumulates into and what RCCL reduces).  Consequences:
+
+* the optimizer is a single fused HIP kernel over ``numel`` elements, not a
+  multi-tensor launch per parameter;
+* data-parallel gradient buckets are contiguous *slices* of the gradient
+  arena -- an all-reduce needs no copy-in/copy-out;
+* every parameter starts at a multiple of ``ALIGN`` elements, so the fused
+  AdamW kernel can look up a parameter's weight-decay flag per 2048-element
+  chunk with one byte load.
+
+Parameters are laid out in *reverse* module-registration order, which is
+approximately the order backward produces their gradients, so the gradient
+buckets at the front of the arena fill first (see ``parallel/ddp.py``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+ALIGN = 2048  # elements; also the AdamW weight-decay chunk size
+
+
+def _round_up(n, a):
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class ParamSlot:
+    name: str
+    param: nn.Parameter
+    offset: int
+    numel: int
+    decay: bool
+
+
+class FlatArena:
+    """Owns the flat param/grad buffers of ``model``; rebinds ``p.data``/``p.grad``."""
+
+    def __init__(self, model: nn.Module, dtype=torch.bfloat16, grad_dtype=None,
+                 device=None, decay_filter=None):
+        device = device or next(model.parameters()).device
+        grad_dtype = grad_dtype or dtype
+        decay_filter = decay_filter or (lambda name, p: p.dim() >= 2)
+        seen = set()
+        named = []
+        for name, p in model.named_parameters():
+            if not p.requires_grad or id(p) in seen:
+                continue
+            seen.add(id(p))
+            named.append((name, p))
+        named.reverse()
+        slots, off = [], 0
+        for name, p in named:
+            slots.append(ParamSlot(name, p, off, p.numel(), bool(decay_filter(name, p))))
+            off = _round_up(off + p.numel(), ALIGN)
+        self.numel = off
+        self.slots = slots
+        self.dtype = dtype
+        self.device = device
+        self.params = torch.zeros(off, dtype=dtype, device=device)
+        self.grads = torch.zeros(off, dtype=grad_dtype, device=device)
+        # per-ALIGN-chunk weight-decay flag (uint8) consumed by the fused AdamW kernel
+        flags = torch.zeros(off // ALIGN, dtype=torch.uint8)
+        for s in slots:
+            if s.decay:
+                flags[s.offset // ALIGN: _round_up(s.offset + s.numel, ALIGN) // ALIGN] = 1
+        self.decay_flags = flags.to(device)
+        with torch.no_grad():
+            for s in slots:
+                view = self.params[s.offset: s.offset + s.numel].view_as(s.param)
+                view.copy_(s.param.data)
+                s.param.data = view
+                s.param.grad = self.grads[s.offset: s.offset + s.numel].view_as(s.param)
+
+    def param_view(self, slot: ParamSlot):
+        return self.params[slot.offset: slot.offset + slot.numel]
+
+    def grad_view(self, slot: ParamSlot):
+        return self.grads[slot.offset: slot.offset + slot.numel]
+
+    def zero_grad(self):
+        self.grads.zero_()
+
+    def rebind_grads(self):
+        """Re-point ``p.grad`` at the arena (after anything replaced it)."""
+        for s in self.slots:
+            g = s.param.grad
+            if g is None or g.data_ptr() != self.grads[s.offset:].data_ptr():
+                s.param.grad = self.grads[s.offset: s.offset + s.numel].view_as(s.param)
+
+    def state_dict_fp32(self, master: torch.Tensor | None = None):
+        src = master if master is not None else self.params
+        return {s.name: src[s.offset: s.offset + s.numel].view(s.param.shape).float().clone()
+                for s in self.slots}
