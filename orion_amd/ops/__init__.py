@@ -110,7 +110,7 @@ def rope(x, cos, sin, pos0=0):
     """Rotate-half RoPE of x (B, T, H, D) at positions pos0..pos0+T-1 (fp32 tables (Tmax, D/2))."""
     b = _gpu(x)
     if b == "hip":
-        from .rope import rope_hip
+        from .rotary import rope_hip
         return rope_hip(x, cos, sin, pos0)
     return ref.rope(x, cos[pos0:], sin[pos0:])
 
@@ -120,7 +120,7 @@ def attention_qkv(qkv, n_head, causal=True):
     """Causal self-attention on a packed (B, T, 3C) projection -> (B, T, C)."""
     b = _gpu(qkv)
     if b == "hip":
-        from .attention import flash_attention_qkv
+        from .flash_attn import flash_attention_qkv
         return flash_attention_qkv(qkv, n_head, causal)
     if b == "torch":
         B, T, C3 = qkv.shape
@@ -136,7 +136,7 @@ def attention(q, k, v, causal=True):
     """Attention on (B, T, H, D) tensors (GQA when k/v have fewer heads)."""
     b = _gpu(q)
     if b == "hip":
-        from .attention import flash_attention
+        from .flash_attn import flash_attention
         return flash_attention(q, k, v, causal)
     if b == "torch":
         rep = q.shape[2] // k.shape[2]

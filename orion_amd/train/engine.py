@@ -62,8 +62,10 @@ class Trainer:
         if ddp:
             from ..parallel.ddp import GradBucketReducer
             self.reducer = GradBucketReducer(self.arena, bucket_mb=bucket_mb)
-            self.reducer.broadcast_params(0)
-            self.opt.master.copy_(self.arena.params)
+            # R1: every rank starts from rank 0's exact fp32 weights
+            dist.broadcast(self.opt.master, 0)
+            with torch.no_grad():
+                self.arena.params.copy_(self.opt.master)
         self.iter_num = 0
 
     def step(self, batches):

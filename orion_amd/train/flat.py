@@ -71,10 +71,14 @@ class FlatArena:
             if s.decay:
                 flags[s.offset // ALIGN: _round_up(s.offset + s.numel, ALIGN) // ALIGN] = 1
         self.decay_flags = flags.to(device)
+        # exact fp32 copy of the initial weights: seeds the optimizer's master weights
+        # (the compute arena itself is rounded to ``dtype``); released by the optimizer
+        self.init_fp32 = torch.zeros(off, dtype=torch.float32, device=device)
         with torch.no_grad():
             for s in slots:
                 view = self.params[s.offset: s.offset + s.numel].view_as(s.param)
                 view.copy_(s.param.data)
+                self.init_fp32[s.offset: s.offset + s.numel].copy_(s.param.data.reshape(-1))
                 s.param.data = view
                 s.param.grad = self.grads[s.offset: s.offset + s.numel].view_as(s.param)
 

@@ -33,7 +33,9 @@ class FlatAdamW:
         self.grad_clip = grad_clip
         self.step_count = 0
         dev = arena.device
-        self.master = arena.params.float().clone()
+        init = getattr(arena, "init_fp32", None)
+        self.master = init if init is not None else arena.params.float().clone()
+        arena.init_fp32 = None
         self.exp_avg = torch.zeros_like(self.master)
         self.exp_avg_sq = torch.zeros_like(self.master)
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
