@@ -45,13 +45,16 @@ def parse():
     ap.add_argument("--grad-accum", type=int, default=2)
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--profile-steps", type=int, default=0,
-                    help="print per-phase timings for this many extra steps (not part of the metric)")
+    ap.add_argument("--no-tuned-gemms", action="store_true",
+                    help="do not load the committed TunableOp GEMM table (orion_amd/tuning/)")
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if not args.no_tuned_gemms:
+        from orion_amd.tuning import use_tuned_gemms
+        use_tuned_gemms()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

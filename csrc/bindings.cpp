@@ -17,14 +17,15 @@
 
 // launchers (csrc/*.hip)
 int orion_layernorm_fwd(const void*, const void*, const void*, void*, float*, float*, int, int,
-                        float, hipStream_t);
+                        float, const void*, void*, hipStream_t);
 int orion_layernorm_bwd_blocks(int rows);
 int orion_layernorm_bwd(const void*, const void*, const void*, const float*, const float*, void*,
-                        void*, void*, float*, int, int, hipStream_t);
+                        void*, void*, float*, int, int, const void*, hipStream_t);
 int orion_colsum_bf16(const void*, void*, float*, int, int, hipStream_t);
 int orion_bias_gelu_fwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_bias_gelu_bwd(const void*, const void*, const void*, void*, float*, int, int, hipStream_t);
-int orion_colsum_partials(const float*, void*, int, int, hipStream_t);
+int orion_colsum_partials2(const float*, float*, void*, int, int, hipStream_t);
+int orion_colsum_scratch(int rows, int C);
 int orion_swiglu_fwd(const void*, void*, long, int, hipStream_t);
 int orion_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_scale_bf16(void*, const float*, long, hipStream_t);
@@ -81,14 +82,45 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& 
   }
   check_launch(orion_layernorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), bp, y.data_ptr(),
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, C,
-                                   (float)eps, cur_stream()),
+                                   (float)eps, nullptr, nullptr, cur_stream()),
                "layernorm_fwd");
   return {y, mean, rstd};
 }
 
+// s = x + r ; y = LayerNorm(s)  -> (s, y, mean, rstd)
+std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, const Tensor& r,
+                                                             const Tensor& w,
+                                                             const c10::optional<Tensor>& b,
+                                                             double eps) {
+  check_bf16(x, "x");
+  check_bf16(r, "residual");
+  check_bf16(w, "weight");
+  TORCH_CHECK(x.sizes() == r.sizes(), "add_layernorm: shape mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto xc = x.contiguous(), rc = r.contiguous();
+  const int C = x.size(-1);
+  const int rows = x.numel() / C;
+  auto y = at::empty_like(xc), sum = at::empty_like(xc);
+  auto opts = x.options().dtype(at::kFloat);
+  auto mean = at::empty({rows}, opts), rstd = at::empty({rows}, opts);
+  const void* bp = nullptr;
+  Tensor bc;
+  if (b.has_value() && b->defined()) {
+    check_bf16(*b, "bias");
+    bc = b->contiguous();
+    bp = bc.data_ptr();
+  }
+  check_launch(orion_layernorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), bp, y.data_ptr(),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, C,
+                                   (float)eps, rc.data_ptr(), sum.data_ptr(), cur_stream()),
+               "add_layernorm_fwd");
+  return {sum, y, mean, rstd};
+}
+
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x,
                                                  const Tensor& w, const Tensor& mean,
-                                                 const Tensor& rstd, bool has_bias) {
+                                                 const Tensor& rstd, bool has_bias,
+                                                 const c10::optional<Tensor>& dres) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto dyc = dy.contiguous(), xc = x.contiguous();
   const int C = x.size(-1);
@@ -97,11 +129,17 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor&
   auto dw = at::empty({C}, w.options());
   Tensor db = has_bias ? at::empty({C}, w.options()) : Tensor();
   const int nb = orion_layernorm_bwd_blocks(rows);
-  auto part = at::empty({2 * (long)nb * C}, x.options().dtype(at::kFloat));
+  auto part = at::empty({2 * (long)nb * C + 32L * C}, x.options().dtype(at::kFloat));
+  Tensor drc;
+  if (dres.has_value() && dres->defined()) {
+    check_bf16(*dres, "dres");
+    drc = dres->contiguous();
+  }
   check_launch(orion_layernorm_bwd(dyc.data_ptr(), xc.data_ptr(), w.contiguous().data_ptr(),
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
                                    dw.data_ptr(), has_bias ? db.data_ptr() : nullptr,
-                                   part.data_ptr<float>(), rows, C, cur_stream()),
+                                   part.data_ptr<float>(), rows, C, drc.defined() ? drc.data_ptr() : nullptr,
+                                   cur_stream()),
                "layernorm_bwd");
   return {dx, dw, db};
 }
@@ -141,15 +179,16 @@ std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& x,
     bp = bc.data_ptr();
     db = at::empty({C}, b->options());
     const int nb = orion_layernorm_bwd_blocks(rows);
-    partt = at::empty({(long)nb * C}, x.options().dtype(at::kFloat));
+    partt = at::empty({(long)orion_colsum_scratch(rows, C)}, x.options().dtype(at::kFloat));
     part = partt.data_ptr<float>();
   }
   check_launch(orion_bias_gelu_bwd(dyc.data_ptr(), xc.data_ptr(), bp, dx.data_ptr(), part, rows,
                                    C, cur_stream()),
                "bias_gelu_bwd");
   if (part) {
-    check_launch(orion_colsum_partials(part, db.data_ptr(), orion_layernorm_bwd_blocks(rows), C,
-                                       cur_stream()),
+    const int nb = orion_layernorm_bwd_blocks(rows);
+    check_launch(orion_colsum_partials2(part, part + (long)nb * C, db.data_ptr(), nb, C,
+                                        cur_stream()),
                  "colsum");
   }
   return {dx, db};
@@ -162,7 +201,7 @@ Tensor colsum(const Tensor& m) {
   const int C = m.size(-1);
   const int rows = m.numel() / C;
   auto out = at::empty({C}, m.options());
-  auto part = at::empty({(long)orion_layernorm_bwd_blocks(rows) * C}, m.options().dtype(at::kFloat));
+  auto part = at::empty({(long)orion_colsum_scratch(rows, C)}, m.options().dtype(at::kFloat));
   check_launch(orion_colsum_bf16(mc.data_ptr(), out.data_ptr(), part.data_ptr<float>(), rows, C,
                                  cur_stream()),
                "colsum");
@@ -273,7 +312,7 @@ std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const 
   const int rows = x.numel() / C;
   auto dx = at::empty_like(xc);
   auto dw = at::empty({C}, w.options());
-  auto part = at::empty({(long)orion_rmsnorm_bwd_blocks(rows) * C}, x.options().dtype(at::kFloat));
+  auto part = at::empty({((long)orion_rmsnorm_bwd_blocks(rows) + 32) * C}, x.options().dtype(at::kFloat));
   check_launch(orion_rmsnorm_bwd(dyc.data_ptr(), xc.data_ptr(), w.contiguous().data_ptr(),
                                  rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr(),
                                  part.data_ptr<float>(), rows, C, cur_stream()),
@@ -380,7 +419,8 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
 
 TORCH_LIBRARY(orion_amd, m) {
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias) -> (Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias, Tensor? dres=None) -> (Tensor, Tensor, Tensor)");
+  m.def("add_layernorm_fwd(Tensor x, Tensor r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor x, Tensor? b) -> Tensor");
   m.def("bias_gelu_bwd(Tensor dy, Tensor x, Tensor? b) -> (Tensor, Tensor)");
   m.def("colsum(Tensor m) -> Tensor");
@@ -400,6 +440,7 @@ TORCH_LIBRARY(orion_amd, m) {
 TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("add_layernorm_fwd", &add_layernorm_fwd);
   m.impl("bias_gelu_fwd", &bias_gelu_fwd);
   m.impl("bias_gelu_bwd", &bias_gelu_bwd);
   m.impl("colsum", &colsum);

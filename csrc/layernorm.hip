@@ -35,7 +35,7 @@ template <int VEC, int ITERS>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    int rows, int C, float eps) {
+    int rows, int C, float eps, const bf16_t* __restrict__ res, bf16_t* __restrict__ sum_out) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -47,6 +47,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const int c = (i * 64 + lane) * VEC;
     if (c < C) {
       load_vec<VEC>(xr + c, v[i]);
+      if (res) {  // fused residual add: s = x + r is both returned and normalised
+        float rv[VEC];
+        load_vec<VEC>(res + (size_t)row * C + c, rv);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) v[i][j] = bf2f(f2bf(v[i][j] + rv[j]));
+        store_vec<VEC>(sum_out + (size_t)row * C + c, v[i]);
+      }
 #pragma unroll
       for (int j = 0; j < VEC; ++j) s += v[i][j];
     } else {
@@ -94,7 +101,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     bf16_t* __restrict__ dx, float* __restrict__ part_dw, float* __restrict__ part_db,
-    int rows, int C, int rows_per_block) {
+    int rows, int C, int rows_per_block, const bf16_t* __restrict__ dres) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float wf[ITERS][VEC], adw[ITERS][VEC], adb[ITERS][VEC];
@@ -148,6 +155,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         float o[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) o[j] = rstd * (g[i][j] - m1 - xh[i][j] * m2);
+        if (dres) {  // gradient arriving through the residual stream
+          float rv[VEC];
+          load_vec<VEC>(dres + (size_t)row * C + c, rv);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) o[j] += rv[j];
+        }
         store_vec<VEC>(dxr + c, o);
       }
     }
@@ -182,23 +195,49 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// out[c] = sum_p part[p][c]  (bf16 output).  Block: 64 columns x 4 row phases.
-__global__ __launch_bounds__(256) void colsum_partials_kernel(
-    const float* __restrict__ part, bf16_t* __restrict__ out, int P, int C) {
+// Two-stage column sum of fp32 partials part[P][C] -> bf16 out[C].
+// Stage 1: grid (ceil(C/64), S); workgroup (s, cblk) folds rows [s*P/S, (s+1)*P/S) of 64
+// columns with 4 waves x 8 independent loads in flight per lane (latency-bound otherwise).
+__global__ __launch_bounds__(256) void colsum_stage1_kernel(const float* __restrict__ part,
+                                                            float* __restrict__ mid, int P, int C,
+                                                            int rows_per_split) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
+  const int p0 = blockIdx.y * rows_per_split, p1 = min(P, p0 + rows_per_split);
   float s = 0.f;
-  if (c < C)
-    for (int p = wv; p < P; p += 4) s += part[(size_t)p * C + c];
+  if (c < C) {
+    int p = p0 + wv;
+    for (; p + 28 < p1; p += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(p + 4 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; p < p1; p += 4) s += part[(size_t)p * C + c];
+  }
   red[wv][lane] = s;
   __syncthreads();
-  if (wv == 0 && c < C) out[c] = f2bf(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+  if (wv == 0 && c < C) mid[(size_t)blockIdx.y * C + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
+
+__global__ __launch_bounds__(256) void colsum_stage2_kernel(const float* __restrict__ mid,
+                                                            bf16_t* __restrict__ out, int S, int C) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int i = 0; i < S; ++i) s += mid[(size_t)i * C + c];
+  out[c] = f2bf(s);
+}
+
+constexpr int COLSUM_SPLITS = 16;
 
 }  // namespace orion
 
 using namespace orion;
+
+int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, hipStream_t st);
 
 static bool ln_pick(int C, int* vec, int* iters) {
   if (C % 8 == 0) {
@@ -216,25 +255,27 @@ static bool ln_pick(int C, int* vec, int* iters) {
 int orion_ln_max_cols() { return 2048; }
 
 int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
-                        float* rstd, int rows, int C, float eps, hipStream_t st) {
+                        float* rstd, int rows, int C, float eps, const void* res, void* sum_out,
+                        hipStream_t st) {
   int vec, it;
   if (!ln_pick(C, &vec, &it)) return -1;
   dim3 grid((rows + 3) / 4), block(256);
   auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto B = (const bf16_t*)b;
   auto Y = (bf16_t*)y;
+  auto R = (const bf16_t*)res; auto S = (bf16_t*)sum_out;
   if (vec == 8) {
     switch (it) {
-      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
-      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
-      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
-      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
     }
   } else {
     switch (it) {
-      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
-      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
-      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
-      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps); break;
+      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
     }
   }
   return (int)hipGetLastError();
@@ -248,7 +289,7 @@ int orion_layernorm_bwd_blocks(int rows) {
 
 int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
                         const float* rstd, void* dx, void* dw, void* db, float* part, int rows,
-                        int C, hipStream_t st) {
+                        int C, const void* dres, hipStream_t st) {
   int vec, it;
   if (!ln_pick(C, &vec, &it)) return -1;
   const int nb = orion_layernorm_bwd_blocks(rows);
@@ -258,24 +299,25 @@ int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const floa
   const size_t lds = (size_t)4 * C * sizeof(float);
   auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w;
   auto DX = (bf16_t*)dx;
+  auto DR = (const bf16_t*)dres;
   if (vec == 8) {
     switch (it) {
-      case 1: ln_bwd_kernel<8, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
-      case 2: ln_bwd_kernel<8, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
-      case 3: ln_bwd_kernel<8, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
-      case 4: ln_bwd_kernel<8, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 1: ln_bwd_kernel<8, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 2: ln_bwd_kernel<8, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 3: ln_bwd_kernel<8, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 4: ln_bwd_kernel<8, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
     }
   } else {
     switch (it) {
-      case 1: ln_bwd_kernel<4, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
-      case 2: ln_bwd_kernel<4, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
-      case 3: ln_bwd_kernel<4, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
-      case 4: ln_bwd_kernel<4, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb); break;
+      case 1: ln_bwd_kernel<4, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 2: ln_bwd_kernel<4, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 3: ln_bwd_kernel<4, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 4: ln_bwd_kernel<4, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
     }
   }
-  const int cb = (C + 63) / 64;
-  if (dw) colsum_partials_kernel<<<cb, 256, 0, st>>>(pdw, (bf16_t*)dw, nb, C);
-  if (db) colsum_partials_kernel<<<cb, 256, 0, st>>>(pdb, (bf16_t*)db, nb, C);
+  float* mid = part + 2 * (size_t)nb * C;
+  if (dw) orion_colsum_partials2(pdw, mid, dw, nb, C, st);
+  if (db) orion_colsum_partials2(pdb, mid + (size_t)COLSUM_SPLITS * C, db, nb, C, st);
   return (int)hipGetLastError();
 }
 
@@ -313,11 +355,19 @@ int orion_colsum_bf16(const void* m, void* out, float* part, int rows, int C, hi
   const int rpb = (rows + nb - 1) / nb;
   dim3 grid(nb, (C / 8 + 63) / 64);
   colsum_bf16_partial_kernel<<<grid, 256, 0, st>>>((const bf16_t*)m, part, rows, C, rpb);
-  colsum_partials_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, (bf16_t*)out, nb, C);
+  orion_colsum_partials2(part, part + (size_t)nb * C, out, nb, C, st);
   return (int)hipGetLastError();
 }
 
-int orion_colsum_partials(const float* part, void* out, int P, int C, hipStream_t st) {
-  colsum_partials_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, (bf16_t*)out, P, C);
+// part[P][C] partials; mid: COLSUM_SPLITS * C floats of scratch
+int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, hipStream_t st) {
+  const int S = P < COLSUM_SPLITS ? (P < 1 ? 1 : P) : COLSUM_SPLITS;
+  const int rps = (P + S - 1) / S;
+  colsum_stage1_kernel<<<dim3((C + 63) / 64, S), 256, 0, st>>>(part, mid, P, C, rps);
+  colsum_stage2_kernel<<<(C + 255) / 256, 256, 0, st>>>(mid, (bf16_t*)out, S, C);
   return (int)hipGetLastError();
+}
+
+int orion_colsum_scratch(int rows, int C) {  // floats of scratch a colsum of `rows` rows needs
+  return (orion_layernorm_bwd_blocks(rows) + 2 * COLSUM_SPLITS) * C;
 }

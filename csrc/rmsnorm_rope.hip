@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ x,
 
 using namespace orion;
 
-int orion_colsum_partials(const float* part, void* out, int P, int C, hipStream_t st);
+int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, hipStream_t st);
 
 static int rms_blocks(int rows) { return rows < 1024 ? rows : 1024; }
 
@@ -197,7 +197,7 @@ int orion_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float*
 #undef RB
     default: return -2;
   }
-  if (dw) return orion_colsum_partials(part, dw, nb, C, st);
+  if (dw) return orion_colsum_partials2(part, part + (size_t)nb * C, dw, nb, C, st);
   return (int)hipGetLastError();
 }
 

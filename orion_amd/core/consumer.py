@@ -1,0 +1,197 @@
+"""Consumer: runs one reserved trial of the user's black box (component C8).
+
+Parity with ``src/orion/core/worker/consumer.py``: in a fresh temporary
+directory the trial's config file (if the user passed a template) and command
+line are rendered, ``METAOPT_RESULTS_PATH`` names a results file, the script is
+executed as a child process, and its JSON results complete the trial; a
+non-zero exit marks it ``broken``.
+
+MI355X-node additions:
+
+* GPU placement: with ``gpus_per_trial = k > 0`` the trial leases k devices
+  from the node's :class:`~orion_amd.core.gpus.GPUSlotPool` and sees them as
+  ``HIP_VISIBLE_DEVICES``; k > 1 trials of a Python script are launched through
+  ``torch.distributed.run --standalone --nproc-per-node k`` (one rank per GPU,
+  RCCL over xGMI);
+* liveness: while the child runs, the trial's ``heartbeat`` is refreshed;
+* ``trial_timeout``: the child is killed and the trial marked ``broken``;
+* SIGINT/SIGTERM of the worker: the child is terminated and the trial is
+  returned to the pool as ``interrupted`` (the reference had the status but
+  never set it);
+* a script that is not executable but ends in ``.py`` runs under the current
+  interpreter (the reference required a shebang + exec bit).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import signal
+import subprocess
+import sys
+import tempfile
+import time
+
+from .trial import Trial
+
+log = logging.getLogger(__name__)
+
+
+class TrialInterrupted(Exception):
+    pass
+
+
+class Consumer:
+    def __init__(self, experiment, gpu_pool=None, gpus_per_trial=0, heartbeat=30.0,
+                 trial_timeout=None, worker_id=None):
+        self.experiment = experiment
+        self.space = experiment.space
+        if self.space is None:
+            raise RuntimeError("Experiment object provided to Consumer has not yet completed "
+                               "initialization.")
+        self.template_builder = experiment.space_builder
+        self.script_path = experiment.metadata["user_script"]
+        self.tmp_dir = os.path.join(tempfile.gettempdir(), "orion")
+        os.makedirs(self.tmp_dir, exist_ok=True)
+        self.gpus_per_trial = int(gpus_per_trial or 0)
+        self.gpu_pool = gpu_pool
+        if self.gpus_per_trial and self.gpu_pool is None:
+            from .gpus import GPUSlotPool
+            self.gpu_pool = GPUSlotPool()
+        self.heartbeat = float(heartbeat or 30.0)
+        self.trial_timeout = trial_timeout
+        self.worker_id = worker_id
+
+    # ------------------------------------------------------------------ public
+    def consume(self, trial):
+        """Evaluate ``trial``; returns the final status string."""
+        with tempfile.TemporaryDirectory(prefix=self.experiment.name + "_", dir=self.tmp_dir) as wd:
+            try:
+                done = self._consume(trial, wd)
+            except TrialInterrupted:
+                log.warning("worker interrupted: trial %s -> interrupted", trial.id)
+                self.experiment.set_trial_status(trial, "interrupted", only_if="reserved")
+                raise KeyboardInterrupt
+        if done is not None:
+            self.experiment.push_completed_trial(done)
+            return "completed"
+        log.debug("### Save %s as broken.", trial)
+        self.experiment.set_trial_status(trial, "broken")
+        return "broken"
+
+    # ------------------------------------------------------------------ internals
+    def _consume(self, trial, workdir):
+        conf = tempfile.NamedTemporaryFile(mode="w", prefix="trial_", suffix=self._conf_suffix(),
+                                           dir=workdir, delete=False)
+        conf.close()
+        res = tempfile.NamedTemporaryFile(mode="w", prefix="results_", suffix=".log", dir=workdir,
+                                          delete=False)
+        res.close()
+        cmd_args = self.template_builder.build_to(conf.name, trial)
+        lease = None
+        if self.gpus_per_trial:
+            lease = self.gpu_pool.acquire(self.gpus_per_trial)
+        try:
+            rc = self._run(res.name, cmd_args, trial, lease)
+        finally:
+            if lease is not None:
+                lease.release()
+        if rc != 0:
+            log.error("Something went wrong. Check logs. Process returned with code %d !", rc)
+            return None
+        try:
+            with open(res.name) as f:
+                results = json.load(f)
+        except (OSError, json.JSONDecodeError) as exc:
+            log.error("trial %s produced no readable results: %s", trial.id, exc)
+            return None
+        if isinstance(results, dict):  # convenience: {"objective": v, ...}
+            results = [dict(name=k, type="objective" if k == "objective" else "constraint", value=v)
+                       for k, v in results.items()]
+        trial.results = [Trial.Result(name=r["name"], type=r["type"], value=r["value"]) for r in results]
+        if trial.objective is None:
+            log.error("trial %s reported no objective", trial.id)
+            return None
+        return trial
+
+    def _conf_suffix(self):
+        cfg = getattr(self.template_builder, "userconfig", None)
+        return os.path.splitext(cfg)[1] if cfg else ".conf"
+
+    def command(self, cmd_args):
+        script = self.script_path
+        if os.access(script, os.X_OK) and not (self.gpus_per_trial > 1 and script.endswith(".py")):
+            base = [script]
+        elif script.endswith(".py"):
+            base = [sys.executable, script]
+        else:
+            base = [script]
+        if self.gpus_per_trial > 1 and script.endswith(".py"):
+            base = [sys.executable, "-m", "torch.distributed.run", "--standalone",
+                    "--local-addr", "127.0.0.1", f"--nproc-per-node={self.gpus_per_trial}", script]
+        return base + list(cmd_args)
+
+    def launch_process(self, results_filename, cmd_args, extra_env=None):
+        env = dict(os.environ)
+        env["METAOPT_RESULTS_PATH"] = str(results_filename)
+        env["ORION_RESULTS_PATH"] = str(results_filename)
+        env["ORION_EXPERIMENT_NAME"] = str(self.experiment.name)
+        env.update(extra_env or {})
+        cmd = self.command(cmd_args)
+        log.debug("launching %s", cmd)
+        try:
+            return subprocess.Popen(cmd, env=env, start_new_session=True)
+        except OSError as exc:
+            log.error("Failed to execute script to evaluate trial: %s", exc)
+            return None
+
+    def _run(self, results_filename, cmd_args, trial, lease):
+        extra = {"ORION_TRIAL_ID": str(trial.id)}
+        if lease is not None:
+            extra.update(lease.env())
+        proc = self.launch_process(results_filename, cmd_args, extra)
+        if proc is None:
+            return -1
+        t0 = time.monotonic()
+        prev = {}
+        interrupted = []
+
+        def _on_signal(signum, _frame):
+            interrupted.append(signum)
+
+        for s in (signal.SIGINT, signal.SIGTERM):
+            try:
+                prev[s] = signal.signal(s, _on_signal)
+            except ValueError:  # not the main thread
+                pass
+        try:
+            while True:
+                try:
+                    return proc.wait(timeout=min(self.heartbeat, 1.0) if interrupted == [] else 0.1)
+                except subprocess.TimeoutExpired:
+                    pass
+                if interrupted:
+                    self._kill(proc)
+                    raise TrialInterrupted()
+                if self.trial_timeout and time.monotonic() - t0 > self.trial_timeout:
+                    log.error("trial %s exceeded its %ss timeout", trial.id, self.trial_timeout)
+                    self._kill(proc)
+                    return -9
+                if time.monotonic() - getattr(self, "_last_beat", 0.0) >= self.heartbeat:
+                    self._last_beat = time.monotonic()
+                    self.experiment.update_heartbeat(trial)
+        finally:
+            for s, h in prev.items():
+                signal.signal(s, h)
+
+    @staticmethod
+    def _kill(proc):
+        try:
+            os.killpg(proc.pid, signal.SIGTERM)
+            proc.wait(timeout=10)
+        except (subprocess.TimeoutExpired, ProcessLookupError, PermissionError):
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+            proc.wait()

@@ -163,9 +163,17 @@ class GPT(nn.Module):
         x = ops.add_broadcast(tok, pos)
         if self.config.dropout and self.training:
             x = F.dropout(x, self.config.dropout)
-        for block in self.transformer.h:
-            x = block(x)
-        x = self.transformer.ln_f(x)
+        # Residual stream with every "x = x + branch; h = LN(x)" pair fused into one kernel
+        # (forward and backward): block i's second add feeds block i+1's ln_1 (ln_f at the end).
+        blocks = self.transformer.h
+        h = blocks[0].ln_1(x)
+        for i, block in enumerate(blocks):
+            a = block.attn(h)
+            x, h = ops.add_layer_norm(x, a, block.ln_2.weight, block.ln_2.bias)
+            m = block.mlp(h)
+            nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else self.transformer.ln_f
+            x, h = ops.add_layer_norm(x, m, nxt.weight, nxt.bias)
+        x = h
         if targets is not None:
             loss = ops.linear_cross_entropy(x.reshape(B * T, -1), self.lm_head.weight,
                                             targets.reshape(-1), ignore_index=-1)

@@ -56,6 +56,16 @@ def layer_norm(x, weight, bias, eps=1e-5):
     return ref.layer_norm(x, weight, bias, eps)
 
 
+def add_layer_norm(x, r, weight, bias, eps=1e-5):
+    """Fused residual add + LayerNorm: returns (s, y) = (x + r, LayerNorm(x + r))."""
+    b = _gpu(x)
+    if b == "hip":
+        from .layernorm import add_layer_norm_hip
+        return add_layer_norm_hip(x, r, weight, bias, eps)
+    s = x + r
+    return s, layer_norm(s, weight, bias, eps)
+
+
 def rms_norm(x, weight, eps=1e-5):
     b = _gpu(x)
     if b == "hip":

@@ -36,6 +36,33 @@ def layer_norm_hip(x, weight, bias, eps=1e-5):
     return _LayerNorm.apply(x, weight, bias, eps)
 
 
+class _AddLayerNorm(torch.autograd.Function):
+    """(s, y) = (x + r, LayerNorm(x + r)); backward folds the residual-stream gradient
+    ds into the LayerNorm input gradient inside the same kernel."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, b, eps):
+        s, y, mean, rstd = C().add_layernorm_fwd(x, r, _bf16(w), _bf16(b), float(eps))
+        ctx.save_for_backward(s, w, mean, rstd)
+        ctx.has_bias = b is not None
+        ctx.b_dtype = None if b is None else b.dtype
+        return s.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, w, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dres = None if ds is None else ds.contiguous()
+        dx, dw, db = C().layernorm_bwd(dy.contiguous(), s, _bf16(w), mean, rstd, ctx.has_bias, dres)
+        dx = dx.view(s.shape)
+        return dx, dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_bias else None), None
+
+
+def add_layer_norm_hip(x, r, weight, bias, eps=1e-5):
+    return _AddLayerNorm.apply(x, r, weight, bias, eps)
+
+
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, eps):
