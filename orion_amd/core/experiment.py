@@ -321,6 +321,8 @@ def create_experiment(name, storage, config, user=None, _retry=True):
     for k in ("database", "resources", "status", "execution"):
         cfg.pop(k, None)
     cfg["name"] = name
+    if not cfg.get("algorithms"):
+        cfg["algorithms"] = "random"  # default optimizer when none is configured
     md = cfg.setdefault("metadata", {})
     md.setdefault("user", exp.metadata["user"])
     md.setdefault("datetime", exp.metadata["datetime"])

@@ -6,6 +6,7 @@
 pick the measured-fastest library kernel per shape with no tuning cost.
 """
 import glob
+import tempfile
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -20,8 +21,27 @@ def use_tuned_gemms(table=None):
         if not tables:
             return None
         table = tables[0]
+    # TunableOp opens "<stem><device ordinal>.csv" when the name has no %d: materialise one
+    # copy per ordinal in a private cache dir so every rank of a multi-GPU job finds it.
+    stem = os.path.splitext(os.path.basename(table))[0]
+    cache = os.path.join(tempfile.gettempdir(), f"orion_amd_tunableop_{os.getuid()}")
+    os.makedirs(cache, exist_ok=True)
+    with open(table, "rb") as f:
+        content = f.read()
+    for ordinal in range(16):
+        dst = os.path.join(cache, f"{stem}{ordinal}.csv")
+        try:
+            with open(dst, "rb") as f:
+                if f.read() == content:
+                    continue
+        except OSError:
+            pass
+        tmpf = f"{dst}.{os.getpid()}.tmp"
+        with open(tmpf, "wb") as f:
+            f.write(content)
+        os.replace(tmpf, dst)
     os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "1"
     os.environ["PYTORCH_TUNABLEOP_TUNING"] = "0"
     os.environ["PYTORCH_TUNABLEOP_RECORD_UNTUNED"] = "0"
-    os.environ["PYTORCH_TUNABLEOP_FILENAME"] = table
+    os.environ["PYTORCH_TUNABLEOP_FILENAME"] = os.path.join(cache, f"{stem}.csv")
     return table

@@ -1,0 +1,230 @@
+"""Algorithms, PrimaryAlgo, Trial, format_trials, client, converters, config
+(reference: tests/unittests/algo/test_base.py, core/test_primary_algo.py,
+core/test_trial.py, core/test_utils_format.py, client/test_client.py,
+core/convert_test.py)."""
+import importlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from orion_amd.algo import BaseAlgorithm, OptimizationAlgorithm, register_algorithm
+from orion_amd.core import config as rc
+from orion_amd.core.format_trials import get_trial_results, trial_to_tuple, tuple_to_trial
+from orion_amd.core.primary_algo import PrimaryAlgo
+from orion_amd.core.trial import Trial
+from orion_amd.io.convert import JSONConverter, YAMLConverter, infer_converter_from_file_type
+from orion_amd.space import SpaceBuilder
+
+
+@pytest.fixture
+def space():
+    return SpaceBuilder().build_from(["-x~uniform(-5, 5)", "--c~choices(['a', 'b'])"])
+
+
+class DumbAlgo(BaseAlgorithm):
+    """Configurable stub recording calls (reference tests/conftest.py:13-70)."""
+
+    def __init__(self, space, value=5, scoring=0, judgement=None, suspend=False, done=False, **nested):
+        super().__init__(space, value=value, scoring=scoring, judgement=judgement,
+                         suspend=suspend, done=done, **nested)
+        self._times_called_suggest = 0
+        self._points, self._results = [], []
+
+    def suggest(self, num=1):
+        self._times_called_suggest += 1
+        return [(self.value, "a")] * num
+
+    def observe(self, points, results):
+        self._points += points
+        self._results += results
+
+    def score(self, point):
+        return self.scoring
+
+    def judge(self, point, measurements):
+        return self.judgement
+
+    @property
+    def should_suspend(self):
+        return self.suspend
+
+    @property
+    def is_done(self):
+        return self.done
+
+
+def test_registry_and_factory(space):
+    assert {"random", "gradient_descent", "dumbalgo"} <= set(OptimizationAlgorithm.typenames)
+    a = OptimizationAlgorithm("DumbAlgo", space, value=1)
+    assert isinstance(a, DumbAlgo) and a.value == 1
+    with pytest.raises(NotImplementedError):
+        OptimizationAlgorithm("nope", space)
+
+
+def test_nested_algorithms_and_configuration(space):
+    a = DumbAlgo(space, value=1, subone={"dumbalgo": {"value": 3}}, subtwo="dumbalgo")
+    assert isinstance(a.subone, DumbAlgo) and a.subone.value == 3 and isinstance(a.subtwo, DumbAlgo)
+    cfg = a.configuration["dumbalgo"]
+    assert cfg["subone"] == {"dumbalgo": dict(value=3, scoring=0, judgement=None, suspend=False, done=False)}
+    new_space = SpaceBuilder().build_from(["-y~uniform(0, 1)"])
+    a.space = new_space
+    assert a.subone.space is new_space
+
+
+def test_random_configuration_parity(space):
+    assert OptimizationAlgorithm("random", space).configuration == {"random": {}}
+    r = OptimizationAlgorithm("random", space, seed=3)
+    assert r.suggest(3) == OptimizationAlgorithm("random", space, seed=3).suggest(3)
+
+
+def test_gradient_descent():
+    s = SpaceBuilder().build_from(["-x~uniform(-50, 50)"])
+    gd = OptimizationAlgorithm("gradient_descent", s, learning_rate=0.1)
+    assert gd.configuration == {"gradient_descent": {"learning_rate": 0.1}}
+    (p,) = gd.suggest()
+    gd.observe([p], [{"objective": 1.0, "gradient": (2.0,)}])
+    assert np.isclose(gd.suggest()[0][0], p[0] - 0.2)
+    assert not gd.is_done
+    gd.observe([p], [{"objective": 1.0, "gradient": (0.0,)}])
+    assert gd.is_done
+
+
+def test_primary_algo_checks(space):
+    pa = PrimaryAlgo(space, {"dumbalgo": {"value": 1}})
+    assert pa.suggest(2) == [(1, "a"), (1, "a")]
+    pa.observe([(1.0, "b")], [{"objective": 3}])
+    assert pa.algorithm._points == [(1.0, "b")]
+    with pytest.raises(AssertionError):
+        pa.observe([(100.0, "b")], [{"objective": 3}])
+    with pytest.raises(AssertionError):
+        pa.observe([(1.0, "b")], [])
+    bad = PrimaryAlgo(space, {"dumbalgo": {"value": 999}})
+    with pytest.raises(AssertionError):
+        bad.suggest()
+    assert pa.configuration == {"dumbalgo": dict(value=1, scoring=0, judgement=None, suspend=False, done=False)}
+    assert pa.score((1.0, "a")) == 0 and pa.judge((1.0, "a"), {}) is None
+    assert pa.is_done is False and pa.should_suspend is False
+
+
+class TestTrial:
+    def test_defaults_and_status(self):
+        t = Trial()
+        assert t.status == "new" and t.params == [] and t.id is None and not t.is_registered
+        with pytest.raises(ValueError):
+            t.status = "running"
+
+    def test_value_types(self):
+        with pytest.raises(ValueError):
+            Trial.Param(name="x", type="float", value=1)
+        with pytest.raises(ValueError):
+            Trial.Result(name="x", type="loss", value=1)
+
+    def test_roundtrip_dict(self):
+        d = dict(_id="abc", experiment="e", status="completed", worker=None,
+                 params=[dict(name="/x", type="real", value=1.0)],
+                 results=[dict(name="o", type="objective", value=2.0),
+                          dict(name="g", type="gradient", value=[1.0])])
+        t = Trial(**d)
+        out = t.to_dict()
+        assert out["_id"] == "abc" and out["params"] == d["params"] and out["results"] == d["results"]
+        assert t.objective.value == 2.0 and t.gradient.value == [1.0]
+
+    def test_first_objective_wins(self):
+        t = Trial(results=[dict(name="a", type="objective", value=1), dict(name="b", type="objective", value=2)])
+        assert t.objective.value == 1
+
+
+def test_format_trials(space):
+    t = tuple_to_trial((np.float64(1.5), "b"), space)
+    assert [p.to_dict() for p in t.params] == [dict(name="/x", type="real", value=1.5),
+                                               dict(name="/c", type="categorical", value="b")]
+    assert trial_to_tuple(t, space) == (1.5, "b")
+    t.results = [Trial.Result(name="o", type="objective", value=1.0),
+                 Trial.Result(name="c", type="constraint", value=2.0)]
+    assert get_trial_results(t) == {"objective": 1.0, "constraint": [2.0], "gradient": None}
+
+
+def test_client_env_contract(tmp_path, monkeypatch, capsys):
+    import orion_amd.client as client
+    monkeypatch.delenv("METAOPT_RESULTS_PATH", raising=False)
+    monkeypatch.delenv("ORION_RESULTS_PATH", raising=False)
+    client = importlib.reload(client)
+    assert not client.IS_METAOPT_ON
+    client.report_results([dict(name="o", type="objective", value=1)])
+    assert "objective" in capsys.readouterr().out
+    with pytest.raises(RuntimeWarning):
+        client.report_results([])
+    path = tmp_path / "res.json"
+    path.write_text("")
+    monkeypatch.setenv("METAOPT_RESULTS_PATH", str(path))
+    client = importlib.reload(client)
+    assert client.IS_METAOPT_ON
+    client.report_results([dict(name="o", type="objective", value=np.float64(2.5))])
+    assert json.loads(path.read_text()) == [dict(name="o", type="objective", value=2.5)]
+    monkeypatch.setenv("METAOPT_RESULTS_PATH", str(tmp_path / "missing.json"))
+    with pytest.raises(RuntimeWarning):
+        importlib.reload(client)
+    monkeypatch.delenv("METAOPT_RESULTS_PATH")
+    importlib.reload(client)
+
+
+def test_orion_compat_import():
+    from orion.client import report_results as r1
+    from orion_amd.client import report_results as r2
+    assert r1.__module__ == r2.__module__
+    from orion.algo.base import BaseAlgorithm as B
+    assert B is BaseAlgorithm
+
+
+def test_converters(tmp_path):
+    data = {"a": [1, 2, {"b": "x"}], "c": 1.5}
+    for ext, klass in ((".yaml", YAMLConverter), (".yml", YAMLConverter), (".json", JSONConverter)):
+        conv = infer_converter_from_file_type("f" + ext)
+        assert isinstance(conv, klass)
+        p = str(tmp_path / ("f" + ext))
+        conv.generate(p, data)
+        assert conv.parse(p) == data
+    with pytest.raises(NotImplementedError):
+        infer_converter_from_file_type("f.ini")
+
+
+class TestConfig:
+    def test_defaults(self, monkeypatch, tmp_path):
+        monkeypatch.setenv("XDG_CONFIG_HOME", str(tmp_path))
+        cfg = rc.fetch_default_options()
+        assert cfg["max_trials"] == float("inf") and cfg["pool_size"] == 10
+        assert cfg["database"]["type"] == "sqlite"
+
+    def test_user_default_file_and_env(self, monkeypatch, tmp_path):
+        monkeypatch.setenv("XDG_CONFIG_HOME", str(tmp_path))
+        d = tmp_path / "orion.core"
+        d.mkdir()
+        (d / "orion_config.yaml").write_text("name: ignored\npool_size: 3\ndatabase:\n  type: memory\n")
+        cfg = rc.fetch_default_options()
+        assert cfg["name"] is None and cfg["pool_size"] == 3 and cfg["database"]["type"] == "memory"
+        monkeypatch.setenv("METAOPT_DB_TYPE", "mongodb")
+        monkeypatch.setenv("ORION_DB_NAME", "x")
+        cfg = rc.merge_env_vars(cfg)
+        assert cfg["database"]["type"] == "mongodb" and cfg["database"]["name"] == "x"
+
+    def test_precedence(self):
+        base = rc.nesteddict()
+        base["pool_size"] = 10
+        base["max_trials"] = 5
+        base["database"]["type"] = "sqlite"
+        merged = rc.merge_orion_config(base, {"max_trials": 7, "pool_size": 8},
+                                       {"max_trials": 9, "database": {"name": "n"}},
+                                       {"max_trials": None, "pool_size": 2, "metadata": {"user_args": []}})
+        assert merged["pool_size"] == 2 and merged["max_trials"] == 9
+        assert merged["database"] == {"type": "sqlite", "name": "n"}
+
+    def test_cli_args(self, tmp_path):
+        cfgf = tmp_path / "o.yaml"
+        cfgf.write_text("name: fromfile\nmax_trials: 4\n")
+        args, cfg = rc.fetch_orion_args(argv=["-n", "x", "--config", str(cfgf), "--workers", "2",
+                                              "script.py", "-x~uniform(0,1)", "--flag"])
+        assert args["name"] == "x" and cfg == {"name": "fromfile", "max_trials": 4}
+        assert args["metadata"]["user_args"] == ["-x~uniform(0,1)", "--flag"]
+        assert args["execution"] == {"workers": 2}

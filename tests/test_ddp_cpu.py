@@ -1,0 +1,81 @@
+"""Data-parallel reducer on CPU with gloo, world_size 2 (SURVEY.md §7.6 tests/dist):
+bucketed, hook-driven all-reduce of the flat gradient arena must equal the
+single-process gradient of the concatenated batch, and the full Trainer must
+keep ranks bit-identical."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as tmp
+
+from orion_amd.models.gpt2 import build_gpt2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, bucket_mb, accum, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    from orion_amd.train.engine import Trainer, OptimConfig
+    model = build_gpt2("gpt2-tiny", block_size=32)
+    tr = Trainer(model, OptimConfig(learning_rate=1e-3, warmup_iters=0, decay_lr=False,
+                                    grad_clip=0.0), bucket_mb=bucket_mb)
+    g = torch.Generator().manual_seed(100)
+    data = [(torch.randint(0, 50257, (4, 32), generator=g), torch.randint(0, 50257, (4, 32), generator=g))
+            for _ in range(world * accum)]
+    mine = [data[rank * accum + j] for j in range(accum)]
+    # capture the reduced gradient before the optimizer by stepping with lr 0 first
+    tr.opt.lr = 0.0
+    tr.arena.zero_grad()
+    for j, (x, y) in enumerate(mine):
+        tr.reducer.set_sync(j == accum - 1)
+        _, loss = model(x, y)
+        (loss / accum).backward()
+    tr.reducer.finish()
+    grads = tr.arena.grads.clone()
+    # then a few real steps; parameters must stay identical across ranks
+    for _ in range(2):
+        tr.step(mine)
+    out.put((rank, grads.numpy(), tr.arena.params.clone().numpy(), len(tr.reducer.buckets)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_mb,accum", [(0.5, 1), (100.0, 2)])
+def test_ddp_matches_single_process(bucket_mb, accum):
+    world = 2
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, accum, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, g0, p0, nb), (_, g1, p1, _) = res
+    g0, g1, p0, p1 = (torch.from_numpy(a) for a in (g0, g1, p0, p1))
+    assert nb >= (2 if bucket_mb < 1 else 1)
+    assert torch.equal(g0, g1)
+    assert torch.equal(p0, p1)
+    # single-process reference gradient over all micro-batches
+    torch.manual_seed(0)
+    from orion_amd.train.flat import FlatArena
+    model = build_gpt2("gpt2-tiny", block_size=32)
+    arena = FlatArena(model, dtype=torch.float32)
+    g = torch.Generator().manual_seed(100)
+    data = [(torch.randint(0, 50257, (4, 32), generator=g), torch.randint(0, 50257, (4, 32), generator=g))
+            for _ in range(world * accum)]
+    arena.zero_grad()
+    for x, y in data:
+        _, loss = model(x, y)
+        (loss / (world * accum)).backward()
+    assert torch.allclose(g0, arena.grads, atol=1e-6, rtol=1e-4)

@@ -1,0 +1,191 @@
+"""Experiment / producer / reservation protocol on local stores
+(reference: tests/unittests/core/test_experiment.py, test_producer.py)."""
+import datetime
+
+import pytest
+
+from orion_amd.core.experiment import Experiment, create_experiment, utcnow
+from orion_amd.core.producer import Producer
+from orion_amd.core.trial import Trial
+from orion_amd.store import Database, DuplicateKeyError
+
+
+@pytest.fixture
+def storage():
+    return Database("memory")
+
+
+def _config(exp, algo=None, args=("-x~uniform(-50, 50)",), max_trials=10, pool_size=2):
+    cfg = exp.configuration
+    cfg["algorithms"] = algo or {"random": {}}
+    cfg["pool_size"] = pool_size
+    cfg["max_trials"] = max_trials
+    cfg["metadata"]["user_script"] = "/bin/true"
+    cfg["metadata"]["user_args"] = list(args)
+    return cfg
+
+
+def test_new_experiment_configure(storage):
+    exp = Experiment("supernaedo", storage, user="tsirif")
+    assert exp.status is None and exp.id is None
+    exp.configure(_config(exp))
+    assert exp.status == "pending" and exp.id is not None
+    doc = storage.read("experiments", {"name": "supernaedo"})[0]
+    assert doc["algorithms"] == {"random": {}} and doc["metadata"]["user"] == "tsirif"
+    assert list(exp.space.keys()) == ["/x"]
+    with pytest.raises(RuntimeError, match="Configuration is done"):
+        exp.configure(_config(exp))
+
+
+def test_resume_same_config(storage):
+    exp = Experiment("e", storage, user="u")
+    exp.configure(_config(exp))
+    exp2 = Experiment("e", storage, user="u")
+    assert exp2.id == exp.id and exp2.status == "pending"
+    cfg = exp2.configuration
+    cfg["max_trials"] = 50  # non-forking attribute: allowed
+    exp2.configure(cfg)
+    assert storage.read("experiments", {"_id": exp.id})[0]["max_trials"] == 50
+    assert storage.count("experiments") == 1
+
+
+def test_fork_is_rejected(storage):
+    exp = Experiment("e", storage, user="u")
+    exp.configure(_config(exp))
+    exp2 = Experiment("e", storage, user="u")
+    cfg = exp2.configuration
+    cfg["metadata"]["user_args"] = ["-x~uniform(0, 1)"]
+    with pytest.raises(NotImplementedError, match="forking"):
+        exp2.configure(cfg)
+
+
+def test_creation_race_duplicate_key(storage):
+    a = Experiment("race", storage, user="u")
+    b = Experiment("race", storage, user="u")
+    a.configure(_config(a))
+    with pytest.raises(DuplicateKeyError):
+        b.configure(_config(b))
+
+
+def test_create_experiment_retries_race(storage):
+    a = Experiment("race2", storage, user="u")
+    a.configure(_config(a))
+    exp = create_experiment("race2", storage, dict(cmdargs={"metadata": {"user_args": ["-x~uniform(-50, 50)"], "user_script": "/bin/true"}, "max_trials": 10, "pool_size": 2}), user="u")
+    assert exp.id == a.id
+
+
+def _ready(storage, **kw):
+    exp = Experiment("w", storage, user="u")
+    exp.configure(_config(exp, **kw))
+    return exp
+
+
+def test_produce_reserve_complete_cycle(storage):
+    exp = _ready(storage)
+    prod = Producer(exp)
+    assert prod.produce() == 2
+    assert exp.count_trials("new") == 2
+    t = exp.reserve_trial(score_handle=prod.algorithm.score, worker="w0")
+    assert t.status == "reserved" and t.start_time is not None and t.worker == "w0"
+    t.results = [Trial.Result(name="o", type="objective", value=3.0)]
+    exp.push_completed_trial(t)
+    got = exp.fetch_completed_trials()
+    assert [x.id for x in got] == [t.id]
+    assert exp.fetch_completed_trials() == []  # incremental
+    assert prod.update() == 0
+    st = exp.stats
+    assert st["trials_completed"] == 1 and st["best_evaluation"] == 3.0 and st["best_trials_id"] == t.id
+
+
+def test_reserve_none_when_empty(storage):
+    exp = _ready(storage)
+    assert exp.reserve_trial() is None
+
+
+def test_reserve_rejects_non_callable(storage):
+    exp = _ready(storage)
+    with pytest.raises(ValueError):
+        exp.reserve_trial(score_handle=5)
+
+
+def test_reserve_lost_race_retries(storage, monkeypatch):
+    """Another worker grabs the chosen trial between read and CAS (reference:
+    patch_sample_concurrent): the loop retries and gets the other one."""
+    exp = _ready(storage)
+    Producer(exp).produce()
+    import random as _r
+    real = _r.sample
+    calls = {"n": 0}
+
+    def sneaky(pop, k):
+        calls["n"] += 1
+        chosen = real(pop, k)
+        if calls["n"] == 1:
+            storage.write("trials", {"status": "reserved"}, {"_id": chosen[0].id})
+        return chosen
+
+    monkeypatch.setattr("orion_amd.core.experiment.random.sample", sneaky)
+    t = exp.reserve_trial()
+    assert t is not None and calls["n"] == 2
+    assert exp.count_trials("reserved") == 2
+
+
+def test_reserve_all_lost_returns_none(storage, monkeypatch):
+    exp = _ready(storage)
+    Producer(exp).produce()
+    import random as _r
+    real = _r.sample
+
+    def always_lose(pop, k):
+        chosen = real(pop, k)
+        storage.write("trials", {"status": "reserved"}, {"_id": chosen[0].id})
+        return chosen
+
+    monkeypatch.setattr("orion_amd.core.experiment.random.sample", always_lose)
+    assert exp.reserve_trial() is None
+
+
+def test_is_done_by_max_trials(storage):
+    exp = _ready(storage, max_trials=2)
+    Producer(exp).produce()
+    for _ in range(2):
+        t = exp.reserve_trial()
+        t.results = [Trial.Result(name="o", type="objective", value=1.0)]
+        exp.push_completed_trial(t)
+    assert exp.is_done
+    assert storage.read("experiments", {"_id": exp.id})[0]["status"] == "done"
+
+
+def test_is_done_by_algorithm(storage):
+    exp = _ready(storage, algo={"gradient_descent": {"learning_rate": 0.1}}, max_trials=100)
+    exp.algorithms.algorithm.gradient = __import__("numpy").array([0.0])
+    assert exp.is_done
+
+
+def test_stats_with_no_completed_trials(storage):
+    exp = _ready(storage)
+    st = exp.stats
+    assert st["trials_completed"] == 0 and st["best_trials_id"] is None
+
+
+def test_stale_reservation_reaper(storage):
+    exp = _ready(storage)
+    Producer(exp).produce()
+    t = exp.reserve_trial()
+    storage.write("trials", {"heartbeat": utcnow() - datetime.timedelta(hours=1)}, {"_id": t.id})
+    assert exp.fix_lost_trials(60) == 1
+    assert storage.read("trials", {"_id": t.id})[0]["status"] == "interrupted"
+    t2 = exp.reserve_trial()  # interrupted trials are reservable again
+    assert t2 is not None
+
+
+def test_fetch_tolerates_clock_skew(storage):
+    """A completed trial stamped slightly before our watermark (other host's slow clock)."""
+    exp = _ready(storage)
+    Producer(exp).produce()
+    exp.fetch_completed_trials()
+    t = exp.reserve_trial()
+    t.results = [Trial.Result(name="o", type="objective", value=1.0)]
+    exp.push_completed_trial(t)
+    storage.write("trials", {"end_time": utcnow() - datetime.timedelta(minutes=2)}, {"_id": t.id})
+    assert [x.id for x in exp.fetch_completed_trials()] == [t.id]

@@ -50,6 +50,26 @@ def test_layernorm_fwd_bwd(C):
     assert rel_err(b.grad, br.grad) < 2e-2
 
 
+def test_add_layernorm_fwd_bwd():
+    torch.manual_seed(0)
+    C = 768
+    x = bf(4, 256, C).requires_grad_()
+    r = bf(4, 256, C).requires_grad_()
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).to(torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).to(torch.bfloat16).requires_grad_()
+    s, y = ops.add_layer_norm(x, r, w, b)
+    ds, dy = bf(4, 256, C), bf(4, 256, C)
+    (s * ds.float()).sum().backward(retain_graph=True)
+    (y.float() * dy.float()).sum().backward()
+    xr, rr, wr, br = (t.detach().float().requires_grad_() for t in (x, r, w, b))
+    sr = xr + rr
+    yr = torch.nn.functional.layer_norm(sr, (C,), wr, br, 1e-5)
+    ((sr * ds.float()).sum() + (yr * dy.float()).sum()).backward()
+    assert rel_err(s, sr) < 1e-2 and rel_err(y, yr) < 1e-2
+    for a, bb in ((x.grad, xr.grad), (r.grad, rr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert rel_err(a, bb) < 2e-2
+
+
 @pytest.mark.parametrize("C", [4096, 2048, 768])
 def test_rmsnorm_fwd_bwd(C):
     torch.manual_seed(0)

@@ -1,0 +1,126 @@
+"""Document-store conformance (memory, SQLite, MongoDB-if-reachable) and a REAL
+multi-process reservation race (reference tests simulated races with patched
+random.sample; SURVEY.md §4 'Improve' item 2)."""
+import datetime
+import multiprocessing as mp
+import os
+
+import pytest
+
+from orion_amd.store import Database, DuplicateKeyError, LocalDB, MemoryDB
+
+
+def _mongo_reachable():
+    try:
+        import pymongo
+        c = pymongo.MongoClient(serverSelectionTimeoutMS=200)
+        c.admin.command("ping")
+        return True
+    except Exception:
+        return False
+
+
+BACKENDS = ["memory", "sqlite"] + (["mongodb"] if _mongo_reachable() else [])
+
+
+@pytest.fixture(params=BACKENDS)
+def db(request, tmp_path):
+    if request.param == "sqlite":
+        return Database("sqlite", host=str(tmp_path / "t.sqlite"))
+    if request.param == "mongodb":
+        d = Database("mongodb", name="orion_amd_test")
+        for c in ("experiments", "trials", "things"):
+            d.drop(c)
+        return d
+    return Database("memory")
+
+
+def test_insert_read_count_remove(db):
+    docs = [{"a": 1, "b": {"c": 2}}, {"a": 2, "b": {"c": 3}}, {"a": 3, "tags": ["x", "y"]}]
+    assert db.write("things", docs) == 3
+    assert all("_id" in d for d in docs)
+    assert db.count("things") == 3
+    assert [d["a"] for d in db.read("things", {"b.c": 3})] == [2]
+    assert sorted(d["a"] for d in db.read("things", {"a": {"$in": [1, 3]}})) == [1, 3]
+    assert sorted(d["a"] for d in db.read("things", {"a": {"$gte": 2}})) == [2, 3]
+    assert [d["a"] for d in db.read("things", {"tags": "x"})] == [3]
+    assert db.count("things", {"a": {"$ne": 1}}) == 2
+    assert db.remove("things", {"a": 1}) == 1
+    assert db.count("things") == 2
+
+
+def test_projection(db):
+    db.write("things", {"a": 1, "b": 2, "c": {"d": 3}})
+    (d,) = db.read("things", {}, selection={"a": 1, "c.d": 1})
+    assert d["a"] == 1 and "b" not in d and d["c"] == {"d": 3} and "_id" in d
+
+
+def test_update_and_upsert(db):
+    db.write("things", {"a": 1, "s": "new"})
+    assert db.write("things", {"s": "old"}, query={"a": 1}) == 1
+    assert db.read("things", {"a": 1})[0]["s"] == "old"
+    db.write("things", {"s": "fresh"}, query={"a": 42})
+    assert db.read("things", {"a": 42})[0]["s"] == "fresh"
+
+
+def test_datetime_roundtrip(db):
+    t = datetime.datetime(2020, 1, 2, 3, 4, 5, 6000)
+    db.write("things", {"t": t})
+    assert db.read("things", {})[0]["t"] == t
+    assert db.count("things", {"t": {"$gte": t}}) == 1
+    assert db.count("things", {"t": {"$gt": t}}) == 0
+
+
+def test_read_and_write_is_cas(db):
+    db.write("things", {"k": 1, "status": "new"})
+    got = db.read_and_write("things", {"k": 1, "status": "new"}, {"status": "reserved"})
+    assert got is not None and got["status"] == "reserved"
+    assert db.read_and_write("things", {"k": 1, "status": "new"}, {"status": "reserved"}) is None
+
+
+def test_unique_index(db):
+    db.ensure_index("experiments", [("name", db.ASCENDING), ("metadata.user", db.ASCENDING)], unique=True)
+    db.write("experiments", {"name": "a", "metadata": {"user": "u"}})
+    db.write("experiments", {"name": "a", "metadata": {"user": "v"}})
+    with pytest.raises(DuplicateKeyError):
+        db.write("experiments", {"name": "a", "metadata": {"user": "u"}})
+
+
+def _racer(path, n_trials, out_q):
+    db = LocalDB(host=path)
+    got = []
+    while True:
+        cands = db.read("trials", {"status": "new"})
+        if not cands:
+            break
+        for c in cands:
+            if db.read_and_write("trials", {"_id": c["_id"], "status": "new"},
+                                 {"status": "reserved", "by": os.getpid()}) is not None:
+                got.append(c["_id"])
+                break
+    out_q.put(got)
+
+
+def test_multiprocess_reservation_race(tmp_path):
+    """N real processes reserve from one SQLite store: every trial exactly once."""
+    path = str(tmp_path / "race.sqlite")
+    db = LocalDB(host=path)
+    n = 120
+    db.write("trials", [{"i": i, "status": "new"} for i in range(n)])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_racer, args=(path, n, q)) for _ in range(4)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    allgot = [x for r in results for x in r]
+    assert len(allgot) == n and len(set(allgot)) == n
+    assert db.count("trials", {"status": "reserved"}) == n
+
+
+def test_factory_names():
+    assert isinstance(Database("memory"), MemoryDB)
+    with pytest.raises(NotImplementedError):
+        Database("nosuchdb")
