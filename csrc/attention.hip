@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
       for (int e = tid; e < BMQ * D; e += 256) {
         const int q = e / D;
         const float sum = dqr[e] + dqr[BMQ * D + e] + dqr[2 * BMQ * D + e] + dqr[3 * BMQ * D + e];
-        if (qbase + q < p.T) atomicAdd(dqg + (long)(qbase + q) * D + (e % D), sum);
+        if (qbase + q < p.T && !(p.flags & 1)) atomicAdd(dqg + (long)(qbase + q) * D + (e % D), sum);
       }
     }
     __syncthreads();

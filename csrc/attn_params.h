@@ -25,6 +25,7 @@ struct AttnParams {
   long dk_sb, dk_st, dk_sh;
   unsigned short* dv;
   long dv_sb, dv_st, dv_sh;
+  int flags;  // diagnostic bits (0 in production): 1 = skip dQ atomics
 };
 
 }  // namespace orion

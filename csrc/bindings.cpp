@@ -17,10 +17,10 @@
 
 // launchers (csrc/*.hip)
 int orion_layernorm_fwd(const void*, const void*, const void*, void*, float*, float*, int, int,
-                        float, const void*, void*, hipStream_t);
+                        float, const void*, void*, const void*, hipStream_t);
 int orion_layernorm_bwd_blocks(int rows);
 int orion_layernorm_bwd(const void*, const void*, const void*, const float*, const float*, void*,
-                        void*, void*, float*, int, int, const void*, hipStream_t);
+                        void*, void*, float*, int, int, const void*, void*, hipStream_t);
 int orion_colsum_bf16(const void*, void*, float*, int, int, hipStream_t);
 int orion_bias_gelu_fwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_bias_gelu_bwd(const void*, const void*, const void*, void*, float*, int, int, hipStream_t);
@@ -82,7 +82,7 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& 
   }
   check_launch(orion_layernorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), bp, y.data_ptr(),
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, C,
-                                   (float)eps, nullptr, nullptr, cur_stream()),
+                                   (float)eps, nullptr, nullptr, nullptr, cur_stream()),
                "layernorm_fwd");
   return {y, mean, rstd};
 }
@@ -91,7 +91,8 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& 
 std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, const Tensor& r,
                                                              const Tensor& w,
                                                              const c10::optional<Tensor>& b,
-                                                             double eps) {
+                                                             double eps,
+                                                             const c10::optional<Tensor>& rbias) {
   check_bf16(x, "x");
   check_bf16(r, "residual");
   check_bf16(w, "weight");
@@ -104,23 +105,29 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, co
   auto opts = x.options().dtype(at::kFloat);
   auto mean = at::empty({rows}, opts), rstd = at::empty({rows}, opts);
   const void* bp = nullptr;
-  Tensor bc;
+  Tensor bc, rbc;
   if (b.has_value() && b->defined()) {
     check_bf16(*b, "bias");
     bc = b->contiguous();
     bp = bc.data_ptr();
   }
+  if (rbias.has_value() && rbias->defined()) {
+    check_bf16(*rbias, "branch bias");
+    rbc = rbias->contiguous();
+  }
   check_launch(orion_layernorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), bp, y.data_ptr(),
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, C,
-                                   (float)eps, rc.data_ptr(), sum.data_ptr(), cur_stream()),
+                                   (float)eps, rc.data_ptr(), sum.data_ptr(),
+                                   rbc.defined() ? rbc.data_ptr() : nullptr, cur_stream()),
                "add_layernorm_fwd");
   return {sum, y, mean, rstd};
 }
 
-std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x,
-                                                 const Tensor& w, const Tensor& mean,
-                                                 const Tensor& rstd, bool has_bias,
-                                                 const c10::optional<Tensor>& dres) {
+std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x,
+                                                         const Tensor& w, const Tensor& mean,
+                                                         const Tensor& rstd, bool has_bias,
+                                                         const c10::optional<Tensor>& dres,
+                                                         bool want_dx_colsum) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto dyc = dy.contiguous(), xc = x.contiguous();
   const int C = x.size(-1);
@@ -129,7 +136,8 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor&
   auto dw = at::empty({C}, w.options());
   Tensor db = has_bias ? at::empty({C}, w.options()) : Tensor();
   const int nb = orion_layernorm_bwd_blocks(rows);
-  auto part = at::empty({2 * (long)nb * C + 32L * C}, x.options().dtype(at::kFloat));
+  auto part = at::empty({3 * (long)nb * C + 48L * C}, x.options().dtype(at::kFloat));
+  Tensor dxs = want_dx_colsum ? at::empty({C}, x.options()) : Tensor();
   Tensor drc;
   if (dres.has_value() && dres->defined()) {
     check_bf16(*dres, "dres");
@@ -139,9 +147,9 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor&
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
                                    dw.data_ptr(), has_bias ? db.data_ptr() : nullptr,
                                    part.data_ptr<float>(), rows, C, drc.defined() ? drc.data_ptr() : nullptr,
-                                   cur_stream()),
+                                   want_dx_colsum ? dxs.data_ptr() : nullptr, cur_stream()),
                "layernorm_bwd");
-  return {dx, dw, db};
+  return {dx, dw, db, dxs};
 }
 
 // ------------------------------------------------------------------ activations
@@ -386,7 +394,7 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
 // dq/dk/dv: preallocated outputs (may be strided views of one packed buffer)
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
               const Tensor& o, const Tensor& lse, bool causal, double scale, Tensor dq, Tensor dk,
-              Tensor dv) {
+              Tensor dv, int64_t flags) {
   check_attn_inputs(q, k, v);
   check_bf16(dout, "dout");
   TORCH_CHECK(dout.stride(3) == 1 && o.stride(3) == 1, "dout/o head dim must be contiguous");
@@ -409,6 +417,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   p.dk_sb = dk.stride(0); p.dk_st = dk.stride(1); p.dk_sh = dk.stride(2);
   p.dv = (unsigned short*)dv.data_ptr();
   p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
+  p.flags = (int)flags;
   check_launch(orion_attn_bwd(p, D, causal, delta.data_ptr<float>(), cur_stream()), "attn_bwd");
   check_launch(orion_attn_dq_convert(dq_acc.data_ptr<float>(), dq.data_ptr(), dq.stride(0),
                                      dq.stride(1), dq.stride(2), p.B, p.Hq, p.T, D, cur_stream()),
@@ -419,8 +428,8 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
 
 TORCH_LIBRARY(orion_amd, m) {
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias, Tensor? dres=None) -> (Tensor, Tensor, Tensor)");
-  m.def("add_layernorm_fwd(Tensor x, Tensor r, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias, Tensor? dres=None, bool want_dx_colsum=False) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("add_layernorm_fwd(Tensor x, Tensor r, Tensor w, Tensor? b, float eps, Tensor? rbias=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor x, Tensor? b) -> Tensor");
   m.def("bias_gelu_bwd(Tensor dy, Tensor x, Tensor? b) -> (Tensor, Tensor)");
   m.def("colsum(Tensor m) -> Tensor");
@@ -434,7 +443,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd) -> (Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int pos0, float sign) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int flags=0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {

@@ -87,18 +87,28 @@ ORION_DEVICE float block_max(float v, float* scratch) {
 }
 
 // GELU (tanh approximation) and its derivative, as in GPT-2 / nanoGPT.
-ORION_DEVICE float gelu_tanh_f(float x) {
+// 0.5 (1 + tanh(u)) == sigmoid(2u) = 1 / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32
+// instead of a tanhf expansion (the activation kernels are HBM-bound only if the VALU keeps up).
+ORION_DEVICE float sigmoid2u_(float x, float* x2out) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  const float m2log2e = -2.8853900817779268f;  // -2 * log2(e)
+  const float x2 = x * x;
+  *x2out = x2;
+  const float u = k0 * fmaf(k1 * x2, x, x);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * m2log2e));
+}
+
+ORION_DEVICE float gelu_tanh_f(float x) {
+  float x2;
+  return x * sigmoid2u_(x, &x2);
 }
 
 ORION_DEVICE float gelu_tanh_grad_f(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  float x2;
+  const float s = sigmoid2u_(x, &x2);
+  // d/dx [x s(2u)] = s + x * 2 s (1 - s) * u'(x),  u' = k0 (1 + 3 k1 x^2)
+  return fmaf(x * 2.f * s * (1.f - s), k0 * fmaf(3.f * k1, x2, 1.f), s);
 }
 
 ORION_DEVICE float silu_f(float x) { return x / (1.f + __expf(-x)); }

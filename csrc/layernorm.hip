@@ -35,7 +35,8 @@ template <int VEC, int ITERS>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    int rows, int C, float eps, const bf16_t* __restrict__ res, bf16_t* __restrict__ sum_out) {
+    int rows, int C, float eps, const bf16_t* __restrict__ res, bf16_t* __restrict__ sum_out,
+    const bf16_t* __restrict__ rbias) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -50,6 +51,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
       if (res) {  // fused residual add: s = x + r is both returned and normalised
         float rv[VEC];
         load_vec<VEC>(res + (size_t)row * C + c, rv);
+        if (rbias) {  // the branch's output-projection bias, added here instead of in the GEMM
+          float bv[VEC];
+          load_vec<VEC>(rbias + c, bv);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) rv[j] = bf2f(f2bf(rv[j] + bv[j]));
+        }
 #pragma unroll
         for (int j = 0; j < VEC; ++j) v[i][j] = bf2f(f2bf(v[i][j] + rv[j]));
         store_vec<VEC>(sum_out + (size_t)row * C + c, v[i]);
@@ -101,10 +108,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     bf16_t* __restrict__ dx, float* __restrict__ part_dw, float* __restrict__ part_db,
-    int rows, int C, int rows_per_block, const bf16_t* __restrict__ dres) {
+    int rows, int C, int rows_per_block, const bf16_t* __restrict__ dres,
+    float* __restrict__ part_dx) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float wf[ITERS][VEC], adw[ITERS][VEC], adb[ITERS][VEC];
+  float wf[ITERS][VEC], adw[ITERS][VEC], adb[ITERS][VEC], adx[ITERS][VEC];
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
     const int c = (i * 64 + lane) * VEC;
@@ -114,7 +122,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       for (int j = 0; j < VEC; ++j) wf[i][j] = 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) { adw[i][j] = 0.f; adb[i][j] = 0.f; }
+    for (int j = 0; j < VEC; ++j) { adw[i][j] = 0.f; adb[i][j] = 0.f; adx[i][j] = 0.f; }
   }
   const float invC = 1.f / (float)C;
   const int r0 = blockIdx.x * rows_per_block;
@@ -161,6 +169,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
           for (int j = 0; j < VEC; ++j) o[j] += rv[j];
         }
+        if (part_dx) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) adx[i][j] += bf2f(f2bf(o[j]));
+        }
         store_vec<VEC>(dxr + c, o);
       }
     }
@@ -192,6 +204,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256)
       part_db[(size_t)blockIdx.x * C + c] = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
+    __syncthreads();
+  }
+  if (part_dx) {
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (c < C) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) red[wv * C + c + j] = adx[i][j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256)
+      part_dx[(size_t)blockIdx.x * C + c] = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
   }
 }
 
@@ -256,26 +282,26 @@ int orion_ln_max_cols() { return 2048; }
 
 int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
                         float* rstd, int rows, int C, float eps, const void* res, void* sum_out,
-                        hipStream_t st) {
+                        const void* rbias, hipStream_t st) {
   int vec, it;
   if (!ln_pick(C, &vec, &it)) return -1;
   dim3 grid((rows + 3) / 4), block(256);
   auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto B = (const bf16_t*)b;
   auto Y = (bf16_t*)y;
-  auto R = (const bf16_t*)res; auto S = (bf16_t*)sum_out;
+  auto R = (const bf16_t*)res; auto S = (bf16_t*)sum_out; auto RB = (const bf16_t*)rbias;
   if (vec == 8) {
     switch (it) {
-      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
-      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
-      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
-      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
     }
   } else {
     switch (it) {
-      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
-      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
-      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
-      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S); break;
+      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
     }
   }
   return (int)hipGetLastError();
@@ -289,35 +315,37 @@ int orion_layernorm_bwd_blocks(int rows) {
 
 int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
                         const float* rstd, void* dx, void* dw, void* db, float* part, int rows,
-                        int C, const void* dres, hipStream_t st) {
+                        int C, const void* dres, void* drbias, hipStream_t st) {
   int vec, it;
   if (!ln_pick(C, &vec, &it)) return -1;
   const int nb = orion_layernorm_bwd_blocks(rows);
   const int rpb = (rows + nb - 1) / nb;
   float* pdw = dw ? part : nullptr;
   float* pdb = db ? part + (size_t)nb * C : nullptr;
+  float* pdx = drbias ? part + 2 * (size_t)nb * C : nullptr;
   const size_t lds = (size_t)4 * C * sizeof(float);
   auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w;
   auto DX = (bf16_t*)dx;
   auto DR = (const bf16_t*)dres;
   if (vec == 8) {
     switch (it) {
-      case 1: ln_bwd_kernel<8, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
-      case 2: ln_bwd_kernel<8, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
-      case 3: ln_bwd_kernel<8, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
-      case 4: ln_bwd_kernel<8, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 1: ln_bwd_kernel<8, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 2: ln_bwd_kernel<8, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 3: ln_bwd_kernel<8, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 4: ln_bwd_kernel<8, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
     }
   } else {
     switch (it) {
-      case 1: ln_bwd_kernel<4, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
-      case 2: ln_bwd_kernel<4, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
-      case 3: ln_bwd_kernel<4, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
-      case 4: ln_bwd_kernel<4, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR); break;
+      case 1: ln_bwd_kernel<4, 1><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 2: ln_bwd_kernel<4, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 3: ln_bwd_kernel<4, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 4: ln_bwd_kernel<4, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
     }
   }
-  float* mid = part + 2 * (size_t)nb * C;
+  float* mid = part + 3 * (size_t)nb * C;
   if (dw) orion_colsum_partials2(pdw, mid, dw, nb, C, st);
   if (db) orion_colsum_partials2(pdb, mid + (size_t)COLSUM_SPLITS * C, db, nb, C, st);
+  if (drbias) orion_colsum_partials2(pdx, mid + 2 * (size_t)COLSUM_SPLITS * C, drbias, nb, C, st);
   return (int)hipGetLastError();
 }
 

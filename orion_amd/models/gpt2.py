@@ -73,10 +73,11 @@ class CausalSelfAttention(nn.Module):
         self.n_head = cfg.n_head
         self.dropout = cfg.dropout
 
-    def forward(self, x):
-        qkv = self.c_attn(x)                       # (B, T, 3C)
-        y = ops.attention_qkv(qkv, self.n_head, causal=True)   # (B, T, C)
-        y = self.c_proj(y)
+    def forward(self, x, fuse_out_bias=False):
+        qkv = ops.linear(x, self.c_attn.weight, self.c_attn.bias)     # (B, T, 3C)
+        y = ops.attention_qkv(qkv, self.n_head, causal=True)         # (B, T, C)
+        # with fuse_out_bias the caller adds c_proj.bias inside its add+LayerNorm kernel
+        y = ops.linear(y, self.c_proj.weight, None if fuse_out_bias else self.c_proj.bias)
         if self.dropout and self.training:
             y = F.dropout(y, self.dropout)
         return y
@@ -89,12 +90,12 @@ class MLP(nn.Module):
         self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd, bias=cfg.bias)
         self.dropout = cfg.dropout
 
-    def forward(self, x):
+    def forward(self, x, fuse_out_bias=False):
         if self.c_fc.bias is not None:
             h = ops.bias_gelu(F.linear(x, self.c_fc.weight), self.c_fc.bias)
         else:
             h = ops.gelu(F.linear(x, self.c_fc.weight))
-        y = self.c_proj(h)
+        y = ops.linear(h, self.c_proj.weight, None if fuse_out_bias else self.c_proj.bias)
         if self.dropout and self.training:
             y = F.dropout(y, self.dropout)
         return y
@@ -165,14 +166,18 @@ class GPT(nn.Module):
             x = F.dropout(x, self.config.dropout)
         # Residual stream with every "x = x + branch; h = LN(x)" pair fused into one kernel
         # (forward and backward): block i's second add feeds block i+1's ln_1 (ln_f at the end).
+        # The branch output-projection biases are folded into the same kernel
+        # (forward: added before the residual sum; backward: their gradient is a
+        # column sum of the residual-stream gradient the kernel already holds).
         blocks = self.transformer.h
         h = blocks[0].ln_1(x)
         for i, block in enumerate(blocks):
-            a = block.attn(h)
-            x, h = ops.add_layer_norm(x, a, block.ln_2.weight, block.ln_2.bias)
-            m = block.mlp(h)
+            a = block.attn(h, fuse_out_bias=True)
+            x, h = ops.add_layer_norm(x, a, block.ln_2.weight, block.ln_2.bias,
+                                      r_bias=block.attn.c_proj.bias)
+            m = block.mlp(h, fuse_out_bias=True)
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else self.transformer.ln_f
-            x, h = ops.add_layer_norm(x, m, nxt.weight, nxt.bias)
+            x, h = ops.add_layer_norm(x, m, nxt.weight, nxt.bias, r_bias=block.mlp.c_proj.bias)
         x = h
         if targets is not None:
             loss = ops.linear_cross_entropy(x.reshape(B * T, -1), self.lm_head.weight,

@@ -56,14 +56,26 @@ def layer_norm(x, weight, bias, eps=1e-5):
     return ref.layer_norm(x, weight, bias, eps)
 
 
-def add_layer_norm(x, r, weight, bias, eps=1e-5):
-    """Fused residual add + LayerNorm: returns (s, y) = (x + r, LayerNorm(x + r))."""
+def add_layer_norm(x, r, weight, bias, eps=1e-5, r_bias=None):
+    """Fused residual add + LayerNorm: (s, y) = (x + r [+ r_bias], LayerNorm(s)).
+    ``r_bias`` is the bias of the branch's output projection (fused here)."""
     b = _gpu(x)
     if b == "hip":
         from .layernorm import add_layer_norm_hip
-        return add_layer_norm_hip(x, r, weight, bias, eps)
+        return add_layer_norm_hip(x, r, weight, bias, eps, r_bias)
+    if r_bias is not None:
+        r = r + r_bias.to(r.dtype)
     s = x + r
     return s, layer_norm(s, weight, bias, eps)
+
+
+def linear(x, weight, bias=None):
+    """x W^T + b (hipBLASLt GEMM; bias gradient by the HIP column-sum kernel)."""
+    b = _gpu(x)
+    if b == "hip":
+        from .layernorm import linear_hip
+        return linear_hip(x, weight, bias)
+    return F.linear(x, weight.to(x.dtype), None if bias is None else bias.to(x.dtype))
 
 
 def rms_norm(x, weight, eps=1e-5):

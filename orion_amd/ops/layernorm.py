@@ -26,8 +26,8 @@ class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xb, w, mean, rstd = ctx.saved_tensors
-        dx, dw, db = C().layernorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), mean, rstd,
-                                       ctx.has_bias)
+        dx, dw, db, _ = C().layernorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), mean, rstd,
+                                          ctx.has_bias)
         dx = dx.view(xb.shape).to(ctx.x_dtype)
         return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_bias else None), None
 
@@ -37,15 +37,18 @@ def layer_norm_hip(x, weight, bias, eps=1e-5):
 
 
 class _AddLayerNorm(torch.autograd.Function):
-    """(s, y) = (x + r, LayerNorm(x + r)); backward folds the residual-stream gradient
-    ds into the LayerNorm input gradient inside the same kernel."""
+    """(s, y) = (x + (r + rb), LayerNorm(s)).  ``rb`` is the bias of the branch's output
+    projection (added here instead of in the GEMM epilogue).  Backward folds the
+    residual-stream gradient ds into the LayerNorm input gradient and produces the
+    branch-bias gradient colsum(ds_total) in the same kernel."""
 
     @staticmethod
-    def forward(ctx, x, r, w, b, eps):
-        s, y, mean, rstd = C().add_layernorm_fwd(x, r, _bf16(w), _bf16(b), float(eps))
+    def forward(ctx, x, r, w, b, rb, eps):
+        s, y, mean, rstd = C().add_layernorm_fwd(x, r, _bf16(w), _bf16(b), float(eps), _bf16(rb))
         ctx.save_for_backward(s, w, mean, rstd)
         ctx.has_bias = b is not None
         ctx.b_dtype = None if b is None else b.dtype
+        ctx.rb_dtype = None if rb is None else rb.dtype
         return s.view(x.shape), y.view(x.shape)
 
     @staticmethod
@@ -54,13 +57,44 @@ class _AddLayerNorm(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros_like(s)
         dres = None if ds is None else ds.contiguous()
-        dx, dw, db = C().layernorm_bwd(dy.contiguous(), s, _bf16(w), mean, rstd, ctx.has_bias, dres)
+        want_rb = ctx.rb_dtype is not None
+        dx, dw, db, drb = C().layernorm_bwd(dy.contiguous(), s, _bf16(w), mean, rstd,
+                                            ctx.has_bias, dres, want_rb)
         dx = dx.view(s.shape)
-        return dx, dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_bias else None), None
+        return (dx, dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_bias else None),
+                (drb.to(ctx.rb_dtype) if want_rb else None), None)
 
 
-def add_layer_norm_hip(x, r, weight, bias, eps=1e-5):
-    return _AddLayerNorm.apply(x, r, weight, bias, eps)
+def add_layer_norm_hip(x, r, weight, bias, eps=1e-5, r_bias=None):
+    return _AddLayerNorm.apply(x, r, weight, bias, r_bias, eps)
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T + b on hipBLASLt; backward computes the bias gradient with the
+    deterministic two-stage column-sum kernel instead of a generic reduction."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = dy2.t() @ x.reshape(-1, x.shape[-1])
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = C().colsum(dy2.contiguous())
+        return dx, dw, db
+
+
+def linear_hip(x, weight, bias=None):
+    return _Linear.apply(x, weight, bias)
 
 
 class _RMSNorm(torch.autograd.Function):
