@@ -168,6 +168,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
 
   gload(0);
   swrite(0);
+  // Retire EVERY prologue load (Q fragments included) with an s_waitcnt the compiler's
+  // wait-count pass can see.  Without it the pass treats qf as still in flight at the loop
+  // header and makes the first QK^T MFMAs of every tile wait vmcnt(3..0) -- i.e. on the
+  // NEXT tile's prefetch -- exposing a full HBM round trip per tile.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) gload(t + 1);
@@ -177,12 +182,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
     const bool active = !CAUSAL || (k0 <= qw0 + 31 + off);
     if (active) {
       f32x16 s[2];
+      bf16x8 kfr[2][D / 16];  // all K fragments of the tile: reads issue back to back
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks)
+          kfr[kb][ks] = lds_b128(Ks, loff<D>(kb * 32 + l32, ks * 16 + 8 * h32));
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         s[kb] = zero16();
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks)
-          s[kb] = mfma32(lds_b128(Ks, loff<D>(kb * 32 + l32, ks * 16 + 8 * h32)), qf[ks], s[kb]);
+        for (int ks = 0; ks < D / 16; ++ks) s[kb] = mfma32(kfr[kb][ks], qf[ks], s[kb]);
       }
       const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw0 + off)) || (k0 + BN > p.Tk);
       if (need_mask) {
@@ -221,12 +231,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
 #pragma unroll
-      for (int db = 0; db < D / 32; ++db)
+      for (int db = 0; db < D / 32; ++db) {
+        bf16x8 vfr[4];
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const bf16x8 a = tr_frag<D>(Vs, kk * 16 + 4 * h32, db * 32, lane, 8);
-          oacc[db] = mfma32(a, pf[kk], oacc[db]);
-        }
+        for (int kk = 0; kk < 4; ++kk) vfr[kk] = tr_frag<D>(Vs, kk * 16 + 4 * h32, db * 32, lane, 8);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) oacc[db] = mfma32(vfr[kk], pf[kk], oacc[db]);
+      }
     }
     if (t + 1 < ntiles) swrite((t + 1) & 1);
     __syncthreads();

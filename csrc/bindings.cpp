@@ -34,10 +34,11 @@ int orion_sumsq_partials();
 int orion_grad_sumsq(const void*, long, float*, float*, hipStream_t);
 int orion_adamw_flat(void*, float*, float*, float*, const void*, const uint8_t*, const float*,
                      const float*, long, hipStream_t);
-int orion_rmsnorm_fwd(const void*, const void*, void*, float*, int, int, float, hipStream_t);
+int orion_rmsnorm_fwd(const void*, const void*, void*, float*, int, int, float, const void*, void*,
+                      hipStream_t);
 int orion_rmsnorm_bwd_blocks(int rows);
 int orion_rmsnorm_bwd(const void*, const void*, const void*, const float*, void*, void*, float*,
-                      int, int, hipStream_t);
+                      int, int, const void*, hipStream_t);
 int orion_rope(const void*, long, long, long, void*, const float*, const float*, int, int, int,
                int, int, float, hipStream_t);
 int orion_attn_fwd(const orion::AttnParams&, int, bool, hipStream_t);
@@ -307,13 +308,34 @@ std::tuple<Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w, double 
   auto y = at::empty_like(xc);
   auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
   check_launch(orion_rmsnorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), y.data_ptr(),
-                                 rstd.data_ptr<float>(), rows, C, (float)eps, cur_stream()),
+                                 rstd.data_ptr<float>(), rows, C, (float)eps, nullptr, nullptr,
+                                 cur_stream()),
                "rmsnorm_fwd");
   return {y, rstd};
 }
 
+// s = x + r ; y = RMSNorm(s) -> (s, y, rstd)
+std::tuple<Tensor, Tensor, Tensor> add_rmsnorm_fwd(const Tensor& x, const Tensor& r, const Tensor& w,
+                                                   double eps) {
+  check_bf16(x, "x");
+  check_bf16(r, "residual");
+  check_bf16(w, "weight");
+  TORCH_CHECK(x.sizes() == r.sizes(), "add_rmsnorm: shape mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto xc = x.contiguous(), rc = r.contiguous();
+  const int C = x.size(-1);
+  const int rows = x.numel() / C;
+  auto y = at::empty_like(xc), sum = at::empty_like(xc);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  check_launch(orion_rmsnorm_fwd(xc.data_ptr(), w.contiguous().data_ptr(), y.data_ptr(),
+                                 rstd.data_ptr<float>(), rows, C, (float)eps, rc.data_ptr(),
+                                 sum.data_ptr(), cur_stream()),
+               "add_rmsnorm_fwd");
+  return {sum, y, rstd};
+}
+
 std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w,
-                                       const Tensor& rstd) {
+                                       const Tensor& rstd, const c10::optional<Tensor>& dres) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto dyc = dy.contiguous(), xc = x.contiguous();
   const int C = x.size(-1);
@@ -321,9 +343,15 @@ std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const 
   auto dx = at::empty_like(xc);
   auto dw = at::empty({C}, w.options());
   auto part = at::empty({((long)orion_rmsnorm_bwd_blocks(rows) + 32) * C}, x.options().dtype(at::kFloat));
+  Tensor drc;
+  if (dres.has_value() && dres->defined()) {
+    check_bf16(*dres, "dres");
+    drc = dres->contiguous();
+  }
   check_launch(orion_rmsnorm_bwd(dyc.data_ptr(), xc.data_ptr(), w.contiguous().data_ptr(),
                                  rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr(),
-                                 part.data_ptr<float>(), rows, C, cur_stream()),
+                                 part.data_ptr<float>(), rows, C,
+                                 drc.defined() ? drc.data_ptr() : nullptr, cur_stream()),
                "rmsnorm_bwd");
   return {dx, dw};
 }
@@ -440,7 +468,8 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
-  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
+  m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int pos0, float sign) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int flags=0) -> ()");
@@ -461,6 +490,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("adamw_flat", &adamw_flat);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.impl("rope", &rope);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);

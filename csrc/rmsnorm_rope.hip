@@ -31,7 +31,9 @@ __global__ __launch_bounds__(256) void rms_fwd_kernel(const bf16_t* __restrict__
                                                       const bf16_t* __restrict__ w,
                                                       bf16_t* __restrict__ y,
                                                       float* __restrict__ rstd_out, int rows,
-                                                      int C, float eps) {
+                                                      int C, float eps,
+                                                      const bf16_t* __restrict__ res,
+                                                      bf16_t* __restrict__ sum_out) {
   __shared__ float red[4];
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     const bf16_t* xr = x + (size_t)row * C;
@@ -42,6 +44,13 @@ __global__ __launch_bounds__(256) void rms_fwd_kernel(const bf16_t* __restrict__
       const int c = (i * 256 + threadIdx.x) * 8;
       if (c < C) {
         ld8f(xr + c, v[i]);
+        if (res) {  // fused residual add: s = x + r returned and normalised
+          float rv[8];
+          ld8f(res + (size_t)row * C + c, rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(v[i][j] + rv[j]));
+          st8f(sum_out + (size_t)row * C + c, v[i]);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += v[i][j] * v[i][j];
       }
@@ -68,7 +77,8 @@ __global__ __launch_bounds__(256) void rms_bwd_kernel(const bf16_t* __restrict__
                                                       const bf16_t* __restrict__ w,
                                                       const float* __restrict__ rstd_in,
                                                       bf16_t* __restrict__ dx,
-                                                      float* __restrict__ part, int rows, int C) {
+                                                      float* __restrict__ part, int rows, int C,
+                                                      const bf16_t* __restrict__ dres) {
   __shared__ float red[4];
   float wf[IT][8], adw[IT][8];
 #pragma unroll
@@ -109,6 +119,12 @@ __global__ __launch_bounds__(256) void rms_bwd_kernel(const bf16_t* __restrict__
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[i][j] - xh[i][j] * m);
+        if (dres) {
+          float rv[8];
+          ld8f(dres + (size_t)row * C + c, rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rv[j];
+        }
         st8f(dx + (size_t)row * C + c, o);
       }
     }
@@ -168,13 +184,14 @@ int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int 
 static int rms_blocks(int rows) { return rows < 1024 ? rows : 1024; }
 
 int orion_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int rows, int C,
-                      float eps, hipStream_t st) {
+                      float eps, const void* res, void* sum_out, hipStream_t st) {
   if (C % 8) return -1;
   const int it = (C / 8 + 255) / 256;
   const int g = rows < 4096 ? rows : 4096;
   auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto Y = (bf16_t*)y;
+  auto R = (const bf16_t*)res; auto S = (bf16_t*)sum_out;
   switch (it) {
-#define RF(K) case K: rms_fwd_kernel<K><<<g, 256, 0, st>>>(X, W, Y, rstd, rows, C, eps); break;
+#define RF(K) case K: rms_fwd_kernel<K><<<g, 256, 0, st>>>(X, W, Y, rstd, rows, C, eps, R, S); break;
     RF(1) RF(2) RF(3) RF(4) RF(5) RF(6) RF(7) RF(8)
 #undef RF
     default: return -2;
@@ -185,14 +202,15 @@ int orion_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int ro
 int orion_rmsnorm_bwd_blocks(int rows) { return rms_blocks(rows); }
 
 int orion_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                      void* dw, float* part, int rows, int C, hipStream_t st) {
+                      void* dw, float* part, int rows, int C, const void* dres, hipStream_t st) {
   if (C % 8) return -1;
   const int it = (C / 8 + 255) / 256;
   const int nb = rms_blocks(rows);
   auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w;
   auto DX = (bf16_t*)dx;
+  auto DR = (const bf16_t*)dres;
   switch (it) {
-#define RB(K) case K: rms_bwd_kernel<K><<<nb, 256, 0, st>>>(DY, X, W, rstd, DX, part, rows, C); break;
+#define RB(K) case K: rms_bwd_kernel<K><<<nb, 256, 0, st>>>(DY, X, W, rstd, DX, part, rows, C, DR); break;
     RB(1) RB(2) RB(3) RB(4) RB(5) RB(6) RB(7) RB(8)
 #undef RB
     default: return -2;

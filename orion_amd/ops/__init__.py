@@ -69,6 +69,16 @@ def add_layer_norm(x, r, weight, bias, eps=1e-5, r_bias=None):
     return s, layer_norm(s, weight, bias, eps)
 
 
+def add_rms_norm(x, r, weight, eps=1e-5):
+    """Fused residual add + RMSNorm: (s, y) = (x + r, RMSNorm(x + r))."""
+    b = _gpu(x)
+    if b == "hip":
+        from .layernorm import add_rms_norm_hip
+        return add_rms_norm_hip(x, r, weight, eps)
+    s = x + r
+    return s, rms_norm(s, weight, eps)
+
+
 def linear(x, weight, bias=None):
     """x W^T + b (hipBLASLt GEMM; bias gradient by the HIP column-sum kernel)."""
     b = _gpu(x)

@@ -109,9 +109,33 @@ class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xb, w, rstd = ctx.saved_tensors
-        dx, dw = C().rmsnorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), rstd)
+        dx, dw = C().rmsnorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), rstd, None)
         return dx.view(xb.shape).to(ctx.x_dtype), dw.to(w.dtype), None
 
 
 def rms_norm_hip(x, weight, eps=1e-5):
     return _RMSNorm.apply(x, weight, eps)
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """(s, y) = (x + r, RMSNorm(x + r)) with the residual gradient folded into backward."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, eps):
+        s, y, rstd = C().add_rmsnorm_fwd(x, r, _bf16(w), float(eps))
+        ctx.save_for_backward(s, w, rstd)
+        return s.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, w, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dres = None if ds is None else ds.contiguous()
+        dx, dw = C().rmsnorm_bwd(dy.contiguous(), s, _bf16(w), rstd, dres)
+        dx = dx.view(s.shape)
+        return dx, dx, dw.to(w.dtype), None
+
+
+def add_rms_norm_hip(x, r, weight, eps=1e-5):
+    return _AddRMSNorm.apply(x, r, weight, eps)
