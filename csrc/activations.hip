@@ -124,6 +124,23 @@ __global__ __launch_bounds__(256) void scale_bf16_kernel(bf16_t* __restrict__ x,
   }
 }
 
+// out[i] = bf16( (*scale) * sum_s slabs[s][i] ): the combine step of the split-K weight
+// gradient (S fp32 slabs from one batched GEMM over token chunks), with the LM head's
+// 1/n_valid * upstream-grad scale folded in.  Fixed summation order: deterministic.
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slabs, int S,
+                                                       long n4, bf16_t* __restrict__ out,
+                                                       const float* __restrict__ scale) {
+  const float sc = scale ? *scale : 1.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4 acc = reinterpret_cast<const f32x4*>(slabs)[i];
+    for (int k = 1; k < S; ++k) acc += reinterpret_cast<const f32x4*>(slabs + (long)k * n4 * 4)[i];
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[j] * sc);
+    reinterpret_cast<bf16x4*>(out)[i] = o;
+  }
+}
+
 }  // namespace orion
 
 using namespace orion;
@@ -173,5 +190,12 @@ int orion_scale_bf16(void* x, const float* scale, long n, hipStream_t st) {
   if (n % 8) return -1;
   const long n8 = n / 8;
   scale_bf16_kernel<<<ew_grid(n8), 256, 0, st>>>((bf16_t*)x, scale, n8);
+  return (int)hipGetLastError();
+}
+
+int orion_slab_sum(const float* slabs, int S, long n, void* out, const float* scale, hipStream_t st) {
+  if (n % 4) return -1;
+  const long n4 = n / 4;
+  slab_sum_kernel<<<ew_grid(n4 / 2), 256, 0, st>>>(slabs, S, n4, (bf16_t*)out, scale);
   return (int)hipGetLastError();
 }

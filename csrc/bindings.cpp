@@ -29,6 +29,7 @@ int orion_colsum_scratch(int rows, int C);
 int orion_swiglu_fwd(const void*, void*, long, int, hipStream_t);
 int orion_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_scale_bf16(void*, const float*, long, hipStream_t);
+int orion_slab_sum(const float*, int, long, void*, const float*, hipStream_t);
 int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
 int orion_sumsq_partials();
 int orion_grad_sumsq(const void*, long, float*, float*, hipStream_t);
@@ -270,6 +271,23 @@ Tensor xent_fwd_bwd(Tensor logits, const Tensor& targets, int64_t ignore_index) 
   return loss;
 }
 
+// split-K combine: slabs (S, ...) fp32 -> bf16 sum over S, optionally times a device scalar
+Tensor slab_sum(const Tensor& slabs, const c10::optional<Tensor>& scale) {
+  TORCH_CHECK(slabs.scalar_type() == at::kFloat && slabs.is_contiguous() && slabs.dim() >= 2,
+              "slab_sum: slabs must be contiguous fp32 (S, ...)");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(slabs.device());
+  const int S = slabs.size(0);
+  auto out = at::empty(slabs.sizes().slice(1), slabs.options().dtype(at::kBFloat16));
+  const float* sc = nullptr;
+  if (scale.has_value() && scale->defined()) {
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "scale must be one fp32");
+    sc = scale->data_ptr<float>();
+  }
+  check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc, cur_stream()),
+               "slab_sum");
+  return out;
+}
+
 // ------------------------------------------------------------------ optimizer
 void grad_sumsq(const Tensor& g, Tensor out) {
   check_bf16(g, "grads");
@@ -464,6 +482,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gu) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
+  m.def("slab_sum(Tensor slabs, Tensor? scale=None) -> Tensor");
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
@@ -485,6 +504,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("scale_", &scale_);
+  m.impl("slab_sum", &slab_sum);
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
   m.impl("grad_sumsq", &grad_sumsq);
   m.impl("adamw_flat", &adamw_flat);

@@ -127,53 +127,70 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   const float invC = 1.f / (float)C;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  for (int row = r0 + wv; row < r1; row += 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    const bf16_t* xr = x + (size_t)row * C;
-    const bf16_t* dyr = dy + (size_t)row * C;
-    float xh[ITERS][VEC], g[ITERS][VEC];
-    float s1 = 0.f, s2 = 0.f;
+  typedef typename VecT<VEC>::type V;
+  // Two rows per wave per iteration, every load of both rows (x, dy, and the
+  // residual-stream gradient) issued before the first reduction: each wave keeps
+  // 2x the bytes in flight and the dres load no longer sits behind the shuffles.
+  constexpr int RU = 2;
+  for (int row = r0 + wv; row < r1; row += 4 * RU) {
+    V xr[RU][ITERS], dyr[RU][ITERS], rr[RU][ITERS];
 #pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const int c = (i * 64 + lane) * VEC;
-      if (c < C) {
-        float xv[VEC], dv[VEC];
-        load_vec<VEC>(xr + c, xv);
-        load_vec<VEC>(dyr + c, dv);
+    for (int u = 0; u < RU; ++u) {
+      const int rw = row + 4 * u;
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-          xh[i][j] = (xv[j] - mean) * rstd;
-          g[i][j] = dv[j] * wf[i][j];
-          s1 += g[i][j];
-          s2 += g[i][j] * xh[i][j];
-          adw[i][j] += dv[j] * xh[i][j];
-          adb[i][j] += dv[j];
+      for (int i = 0; i < ITERS; ++i) {
+        const int c = (i * 64 + lane) * VEC;
+        if (c < C && rw < r1) {
+          xr[u][i] = *reinterpret_cast<const V*>(x + (size_t)rw * C + c);
+          dyr[u][i] = *reinterpret_cast<const V*>(dy + (size_t)rw * C + c);
+          if (dres) rr[u][i] = *reinterpret_cast<const V*>(dres + (size_t)rw * C + c);
         }
-      } else {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) { xh[i][j] = 0.f; g[i][j] = 0.f; }
       }
     }
-    const float m1 = wave_sum(s1) * invC, m2 = wave_sum(s2) * invC;
-    bf16_t* dxr = dx + (size_t)row * C;
 #pragma unroll
-    for (int i = 0; i < ITERS; ++i) {
-      const int c = (i * 64 + lane) * VEC;
-      if (c < C) {
-        float o[VEC];
+    for (int u = 0; u < RU; ++u) {
+      const int rw = row + 4 * u;
+      if (rw >= r1) break;
+      const float mean = mean_in[rw], rstd = rstd_in[rw];
+      float xh[ITERS][VEC], g[ITERS][VEC];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) o[j] = rstd * (g[i][j] - m1 - xh[i][j] * m2);
-        if (dres) {  // gradient arriving through the residual stream
-          float rv[VEC];
-          load_vec<VEC>(dres + (size_t)row * C + c, rv);
+      for (int i = 0; i < ITERS; ++i) {
+        const int c = (i * 64 + lane) * VEC;
+        if (c < C) {
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) o[j] += rv[j];
+          for (int j = 0; j < VEC; ++j) {
+            const float dv = bf2f(dyr[u][i][j]);
+            xh[i][j] = (bf2f(xr[u][i][j]) - mean) * rstd;
+            g[i][j] = dv * wf[i][j];
+            s1 += g[i][j];
+            s2 += g[i][j] * xh[i][j];
+            adw[i][j] += dv * xh[i][j];
+            adb[i][j] += dv;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) { xh[i][j] = 0.f; g[i][j] = 0.f; }
         }
-        if (part_dx) {
+      }
+      const float m1 = wave_sum(s1) * invC, m2 = wave_sum(s2) * invC;
+      bf16_t* dxr = dx + (size_t)rw * C;
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) adx[i][j] += bf2f(f2bf(o[j]));
+      for (int i = 0; i < ITERS; ++i) {
+        const int c = (i * 64 + lane) * VEC;
+        if (c < C) {
+          float o[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) {
+            o[j] = rstd * (g[i][j] - m1 - xh[i][j] * m2);
+            if (dres) o[j] += bf2f(rr[u][i][j]);  // gradient arriving through the residual stream
+          }
+          if (part_dx) {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) adx[i][j] += bf2f(f2bf(o[j]));
+          }
+          store_vec<VEC>(dxr + c, o);
         }
-        store_vec<VEC>(dxr + c, o);
       }
     }
   }
@@ -265,8 +282,15 @@ using namespace orion;
 
 int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, hipStream_t st);
 
-static bool ln_pick(int C, int* vec, int* iters) {
-  if (C % 8 == 0) {
+// exact_fit: 4-wide slices when they tile the row exactly and 8-wide ones would not
+// (C = 768: 3 x 64 x 4 uses every lane, 2 x 64 x 8 leaves a third idle).  Measured on
+// MI355X at 65536 x 768: the backward gains from it, the forward does not (its 16-byte
+// loads win), so only the backward asks for it.
+static bool ln_pick(int C, int* vec, int* iters, bool exact_fit = false) {
+  if (exact_fit && C % 256 == 0 && C % 512 != 0 && C <= 1024) {
+    *vec = 4;
+    *iters = C / 256;
+  } else if (C % 8 == 0) {
     *vec = 8;
     *iters = (C + 511) / 512;
   } else if (C % 4 == 0) {
@@ -317,7 +341,7 @@ int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const floa
                         const float* rstd, void* dx, void* dw, void* db, float* part, int rows,
                         int C, const void* dres, void* drbias, hipStream_t st) {
   int vec, it;
-  if (!ln_pick(C, &vec, &it)) return -1;
+  if (!ln_pick(C, &vec, &it, /*exact_fit=*/true)) return -1;
   const int nb = orion_layernorm_bwd_blocks(rows);
   const int rpb = (rows + nb - 1) / nb;
   float* pdw = dw ? part : nullptr;

@@ -13,23 +13,56 @@
 
 namespace orion {
 
-constexpr int XT = 512;  // threads per row
-constexpr int XW = XT / 64;
 
-// inv_n[0] = 1 / max(1, #targets != ignore_index)
-__global__ __launch_bounds__(256) void count_valid_kernel(const int64_t* __restrict__ t, long N,
-                                                          long ignore, float* __restrict__ inv_n) {
-  __shared__ float red[4];
+// inv_n[0] = 1 / max(1, #targets != ignore_index).  One workgroup; 8 independent
+// loads in flight per thread so the pass is bandwidth- not latency-bound (the
+// previous one-load-at-a-time loop took ~56 us for 32k targets).
+template <typename T>
+__device__ __forceinline__ float n_valid(T v, long ignore);
+template <>
+__device__ __forceinline__ float n_valid<i64x2>(i64x2 v, long ignore) {
+  return (v[0] != ignore ? 1.f : 0.f) + (v[1] != ignore ? 1.f : 0.f);
+}
+template <>
+__device__ __forceinline__ float n_valid<int64_t>(int64_t v, long ignore) {
+  return v != ignore ? 1.f : 0.f;
+}
+
+template <typename T>  // i64x2 when the targets are 16-byte aligned, else int64_t
+__global__ __launch_bounds__(1024) void count_valid_kernel(const int64_t* __restrict__ t, long N,
+                                                           long ignore, float* __restrict__ inv_n) {
+  __shared__ float red[16];
+  constexpr int PER = sizeof(T) / sizeof(int64_t);
+  const long NV = N / PER;
+  const T* tv = reinterpret_cast<const T*>(t);
   float c = 0.f;
-  for (long i = threadIdx.x; i < N; i += 256) c += (t[i] != ignore) ? 1.f : 0.f;
-  c = block_sum<4>(c, red);
+  for (long base = threadIdx.x; base < NV; base += 8 * 1024) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long i = base + u * 1024;
+      if (i < NV) v[u] = tv[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (base + u * 1024 < NV) c += n_valid<T>(v[u], ignore);
+  }
+  if (threadIdx.x == 0)
+    for (long i = NV * PER; i < N; ++i) c += (t[i] != ignore) ? 1.f : 0.f;
+  c = block_sum<16>(c, red);
   if (threadIdx.x == 0) inv_n[0] = 1.f / fmaxf(c, 1.f);
 }
 
-template <int CH>  // 16-byte chunks per thread (CH * 8 * XT >= V)
-__global__ __launch_bounds__(XT) void xent_fwd_bwd_kernel(
+// Occupancy: the row lives in registers (CH x 4 VGPRs), so the VGPR budget decides how
+// many rows a CU streams at once.  Capping at 128 VGPRs (4 waves/SIMD) fits TWO
+// 8-wave workgroups per CU: while one row is in its reduction phase the other is
+// loading/storing, which is what keeps HBM busy (one row per CU left it ~50% idle).
+// Vocabularies over 13 x 4096 use 1024 threads per row so CH stays <= 13.
+template <int CH, int XT>  // 16-byte chunks per thread (CH * 8 * XT >= V)
+__global__ __launch_bounds__(XT, (XT == 512 ? 4 : 2)) void xent_fwd_bwd_kernel(
     bf16_t* __restrict__ logits, const int64_t* __restrict__ targets, float* __restrict__ losses,
     const float* __restrict__ inv_n, int V, long ignore) {
+  constexpr int XW = XT / 64;
   __shared__ float red[XW];
   const long row = blockIdx.x;
   bf16_t* lr = logits + row * (long)V;
@@ -61,10 +94,7 @@ __global__ __launch_bounds__(XT) void xent_fwd_bwd_kernel(
   const float lse = m + __logf(s);
   const float scale = valid ? inv_n[0] : 0.f;
   const float inv_s = 1.f / s;
-  if (threadIdx.x == 0) {
-    losses[row] = valid ? (lse - bf2f(lr[tgt])) : 0.f;
-  }
-  __syncthreads();  // the target logit is read above before anyone overwrites it
+  if (!valid && threadIdx.x == 0) losses[row] = 0.f;
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = k * XT + threadIdx.x;
@@ -73,7 +103,10 @@ __global__ __launch_bounds__(XT) void xent_fwd_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float p = __expf(bf2f(v[k][j]) - m) * inv_s;
-        if (c * 8 + j == tgt) p -= 1.f;
+        if (c * 8 + j == tgt) {  // the owner of the target logit writes the row loss
+          p -= 1.f;
+          losses[row] = lse - bf2f(v[k][j]);
+        }
         o[j] = f2bf(p * scale);
       }
       *reinterpret_cast<bf16x8*>(lr + c * 8) = o;
@@ -87,7 +120,13 @@ __global__ __launch_bounds__(1024) void mean_loss_kernel(const float* __restrict
                                                          float* __restrict__ out) {
   __shared__ float red[16];
   float s = 0.f;
-  for (long i = threadIdx.x; i < N; i += 1024) s += losses[i];
+  for (long base = threadIdx.x; base < N; base += 8 * 1024) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = base + u * 1024 < N ? losses[base + u * 1024] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
   s = block_sum<16>(s, red);
   if (threadIdx.x == 0) out[0] = s * inv_n[0];
 }
@@ -100,16 +139,25 @@ using namespace orion;
 int orion_xent_fwd_bwd(void* logits, const int64_t* targets, float* losses, float* inv_n,
                        float* loss_out, long N, int V, long ignore, hipStream_t st) {
   if (V % 8) return -1;
-  count_valid_kernel<<<1, 256, 0, st>>>(targets, N, ignore, inv_n);
-  const int chunks = (V / 8 + XT - 1) / XT;
+  if ((reinterpret_cast<uintptr_t>(targets) & 15) == 0)
+    count_valid_kernel<i64x2><<<1, 1024, 0, st>>>(targets, N, ignore, inv_n);
+  else
+    count_valid_kernel<int64_t><<<1, 1024, 0, st>>>(targets, N, ignore, inv_n);
   auto L = (bf16_t*)logits;
-  switch (chunks) {
-#define XC(K) case K: xent_fwd_bwd_kernel<K><<<N, XT, 0, st>>>(L, targets, losses, inv_n, V, ignore); break;
-    XC(1) XC(2) XC(3) XC(4) XC(5) XC(6) XC(7) XC(8) XC(9) XC(10) XC(11) XC(12) XC(13) XC(14)
-    XC(15) XC(16) XC(17) XC(18) XC(19) XC(20) XC(21) XC(22) XC(23) XC(24) XC(25) XC(26)
-    XC(27) XC(28) XC(29) XC(30) XC(31) XC(32)
+  const int c512 = (V / 8 + 511) / 512, c1024 = (V / 8 + 1023) / 1024;
+  if (c512 <= 13) {
+    switch (c512) {
+#define XC(K) case K: xent_fwd_bwd_kernel<K, 512><<<N, 512, 0, st>>>(L, targets, losses, inv_n, V, ignore); break;
+      XC(1) XC(2) XC(3) XC(4) XC(5) XC(6) XC(7) XC(8) XC(9) XC(10) XC(11) XC(12) XC(13)
 #undef XC
-    default: return -2;  // V > 131072
+    }
+  } else {
+    switch (c1024) {
+#define XC(K) case K: xent_fwd_bwd_kernel<K, 1024><<<N, 1024, 0, st>>>(L, targets, losses, inv_n, V, ignore); break;
+      XC(7) XC(8) XC(9) XC(10) XC(11) XC(12) XC(13) XC(14) XC(15) XC(16)
+#undef XC
+      default: return -2;  // V > 131072
+    }
   }
   mean_loss_kernel<<<1, 1024, 0, st>>>(losses, N, inv_n, loss_out);
   return (int)hipGetLastError();

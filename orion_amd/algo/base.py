@@ -18,39 +18,18 @@ reference, so existing plugin packages keep working once they import
 from __future__ import annotations
 
 import abc
-import importlib.metadata
 import logging
+
+from ..utils import Registry
 
 log = logging.getLogger(__name__)
 
 ENTRY_POINT_GROUP = "OptimizationAlgorithm"
-_REGISTRY: dict[str, type] = {}
-_EP_LOADED = False
+ALGORITHMS = Registry("BaseAlgorithm", entry_point_group=ENTRY_POINT_GROUP)
 
 
 def register_algorithm(cls, name=None):
-    _REGISTRY[(name or cls.__name__).lower()] = cls
-    return cls
-
-
-def _load_entry_points():
-    global _EP_LOADED
-    if _EP_LOADED:
-        return
-    _EP_LOADED = True
-    try:
-        eps = importlib.metadata.entry_points()
-        group = eps.select(group=ENTRY_POINT_GROUP) if hasattr(eps, "select") else eps.get(ENTRY_POINT_GROUP, [])
-    except Exception as exc:  # pragma: no cover
-        log.debug("entry point discovery failed: %s", exc)
-        return
-    for ep in group:
-        try:
-            obj = ep.load()
-            if isinstance(obj, type) and issubclass(obj, BaseAlgorithm):
-                register_algorithm(obj, ep.name if ep.name.lower() != obj.__name__.lower() else None)
-        except Exception as exc:
-            log.warning("could not load algorithm plugin %s: %s", ep, exc)
+    return ALGORITHMS.register(cls, name=name)
 
 
 class BaseAlgorithm(abc.ABC):
@@ -133,27 +112,21 @@ class BaseAlgorithm(abc.ABC):
         pass
 
 
+ALGORITHMS.base = BaseAlgorithm  # entry points must resolve to BaseAlgorithm subclasses
+
+
 class _FactoryMeta(abc.ABCMeta):
     @property
     def types(cls):
-        _load_entry_points()
-        return list(_REGISTRY.values())
+        return ALGORITHMS.types
 
     @property
     def typenames(cls):
-        _load_entry_points()
-        return list(_REGISTRY.keys())
+        return ALGORITHMS.typenames
 
 
 class OptimizationAlgorithm(metaclass=_FactoryMeta):
     """Factory: ``OptimizationAlgorithm('random', space, **kw)`` -> a ``Random`` instance."""
 
     def __new__(cls, of_type, space, **kwargs):
-        _load_entry_points()
-        key = str(of_type).lower()
-        if key not in _REGISTRY:
-            raise NotImplementedError(
-                "Could not find implementation of BaseAlgorithm, type = '{}'\n"
-                "Currently, there is an implementation for types:\n{}".format(
-                    of_type, sorted(_REGISTRY)))
-        return _REGISTRY[key](space, **kwargs)
+        return ALGORITHMS.create(of_type, space, **kwargs)

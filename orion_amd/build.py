@@ -21,9 +21,9 @@ import sys
 import sysconfig
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CSRC = os.path.join(ROOT, "csrc")
-BUILD = os.path.join(ROOT, "build", "csrc")
-OUT = os.path.join(ROOT, "orion_amd", "_C.so")
+CSRC = os.environ.get("ORION_AMD_CSRC", os.path.join(ROOT, "csrc"))
+BUILD = os.environ.get("ORION_AMD_BUILD_DIR", os.path.join(ROOT, "build", "csrc"))
+OUT = os.environ.get("ORION_AMD_EXT", os.path.join(ROOT, "orion_amd", "_C.so"))
 ARCH = os.environ.get("ORION_AMD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")

@@ -13,6 +13,8 @@ import os
 
 import yaml
 
+from ..utils import Registry
+
 
 class BaseConverter:
     file_extensions: tuple = ()
@@ -48,16 +50,14 @@ class JSONConverter(BaseConverter):
             json.dump(data, f)
 
 
-_CONVERTERS = {"yamlconverter": YAMLConverter, "jsonconverter": JSONConverter}
+CONVERTERS = Registry("BaseConverter")
+CONVERTERS.register(YAMLConverter)
+CONVERTERS.register(JSONConverter)
 
 
 def Converter(of_type, *args, **kwargs):  # noqa: N802  (factory with the reference's name)
     """Instantiate a converter by (case-insensitive) class name."""
-    try:
-        return _CONVERTERS[of_type.lower()](*args, **kwargs)
-    except KeyError as exc:
-        raise NotImplementedError("Could not find implementation of BaseConverter, "
-                                  "type = '{}'".format(of_type)) from exc
+    return CONVERTERS.create(of_type, *args, **kwargs)
 
 
 def infer_converter_from_file_type(config_path, regex=None, default_keyword=""):

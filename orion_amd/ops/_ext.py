@@ -13,7 +13,8 @@ import threading
 import torch
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EXT_PATH = os.path.join(_PKG_DIR, "_C.so")
+# ORION_AMD_EXT selects an alternative build (same-box A/B benchmarking of kernel variants)
+EXT_PATH = os.environ.get("ORION_AMD_EXT", os.path.join(_PKG_DIR, "_C.so"))
 
 _lock = threading.Lock()
 _loaded = False

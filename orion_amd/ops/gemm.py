@@ -1,0 +1,53 @@
+"""Weight-gradient GEMM with explicit split-K over the token dimension.
+
+dW = dY^T X reduces over all B*T tokens (65,536 rows for the GPT-2 bench) into
+a small output (768 x 768 ... 3072 x 768).  A single GEMM of that shape has only
+9-36 output tiles of 256 x 256 for 256 CUs, and hipBLASLt's picks run at
+0.4-0.8 PF/s on MI355X (`scripts/bench_wgrad.py`, profiles/wgrad_r01.json), well
+below the 1.3-1.6 PF/s of the forward GEMMs of the same layers.
+
+Here the token dimension is cut into S chunks and the chunks become the batch of
+ONE batched GEMM with fp32 output (S x more workgroups, no bf16 rounding of the
+partial sums), and a HIP kernel (`slab_sum`, csrc/activations.hip) folds the S
+fp32 slabs into the bf16 gradient in a fixed order, optionally times a device
+scalar (the LM head's loss scale).  Measured on MI355X at M = 65,536:
+768x768 0.20 -> 0.11 ms, 2304x768 0.39 -> 0.27 ms, 768x3072 0.41 -> 0.34 ms.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ._ext import C
+
+_FORCE = os.environ.get("ORION_WGRAD_SPLITS")
+
+
+def wgrad_splits(M: int, n1: int, n2: int) -> int:
+    """How many token chunks to split a (n1 x n2, K = M) weight gradient into."""
+    if _FORCE is not None:
+        s = int(_FORCE)
+        return s if s >= 1 and M % s == 0 else 1
+    tiles = -(-n1 // 256) * -(-n2 // 256)
+    if tiles >= 128:
+        return 1  # enough output tiles already; the fp32 slab round trip would cost more
+    s = 16
+    while s > 1 and (M % s or M // s < 2048 or tiles * s > 1024):
+        s //= 2
+    return s
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Tensor:
+    """dy (M, n1), x (M, n2) bf16 -> dy^T x (n1, n2) bf16 [times the device scalar ``scale``]."""
+    M, n1 = dy.shape
+    n2 = x.shape[1]
+    S = wgrad_splits(M, n1, n2)
+    if S == 1:
+        dw = dy.t() @ x
+        if scale is not None:
+            C().scale_(dw, scale)
+        return dw
+    slabs = torch.bmm(dy.contiguous().view(S, M // S, n1).transpose(1, 2),
+                      x.contiguous().view(S, M // S, n2), out_dtype=torch.float32)
+    return C().slab_sum(slabs, scale)

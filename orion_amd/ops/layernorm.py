@@ -6,6 +6,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
+from .gemm import wgrad
 
 
 def _bf16(t):
@@ -87,7 +88,7 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ w).view(x.shape)
         if ctx.needs_input_grad[1]:
-            dw = dy2.t() @ x.reshape(-1, x.shape[-1])
+            dw = wgrad(dy2, x.reshape(-1, x.shape[-1]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = C().colsum(dy2.contiguous())
         return dx, dw, db

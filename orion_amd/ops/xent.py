@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
+from .gemm import wgrad
 
 
 class _LinearXent(torch.autograd.Function):
@@ -29,8 +30,7 @@ class _LinearXent(torch.autograd.Function):
             dx = dl @ w
             C().scale_(dx, s)
         if ctx.needs_input_grad[1]:
-            dw = dl.t() @ x
-            C().scale_(dw, s)
+            dw = wgrad(dl, x, s)
         return dx, dw, None, None
 
 

@@ -20,21 +20,18 @@ from .local import LocalDB
 from .memory import MemoryDB
 from .mongodb import MongoDB
 
-_BACKENDS = {
-    "sqlite": LocalDB, "local": LocalDB, "localdb": LocalDB, "pickleddb": LocalDB,
-    "memory": MemoryDB, "memorydb": MemoryDB, "ephemeraldb": MemoryDB,
-    "mongodb": MongoDB, "mongo": MongoDB,
-}
+from ..utils import Registry
+
+# third-party backends can join through the "Database" entry-point group
+BACKENDS = Registry("AbstractDB", entry_point_group="Database", base=AbstractDB)
+BACKENDS.register(LocalDB, name="sqlite", aliases=("local", "localdb", "pickleddb"))
+BACKENDS.register(MemoryDB, name="memory", aliases=("memorydb", "ephemeraldb"))
+BACKENDS.register(MongoDB, name="mongodb", aliases=("mongo",))
 
 
 def Database(of_type="sqlite", **options):  # noqa: N802  (reference factory name)
-    try:
-        klass = _BACKENDS[str(of_type).lower()]
-    except KeyError as exc:
-        raise NotImplementedError(f"Could not find implementation of AbstractDB, type = "
-                                  f"'{of_type}' (known: {sorted(set(_BACKENDS))})") from exc
-    return klass(**options)
+    return BACKENDS.create(of_type, **options)
 
 
 def backend_names():
-    return sorted(_BACKENDS)
+    return BACKENDS.typenames

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Same-box A/B of attention kernels: alternate processes base/new, 3 rounds each.
+cd "$(dirname "$0")/.."
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+for r in 1 2 3; do
+  for v in base new; do
+    if [[ $v == base ]]; then ext=$PWD/variants/_C_base.so; else ext=$PWD/orion_amd/_C.so; fi
+    ORION_AMD_EXT=$ext timeout -k 10 120 python scripts/bench_attn.py ${ATTN_ARGS:-} > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
+    echo "$v $(tail -1 gpurun_out/ab_$v.log)"
+  done
+done

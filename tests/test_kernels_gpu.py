@@ -197,7 +197,7 @@ def test_flash_attention_softmax_spike():
     assert rel_err(o, _attn_ref(q, k, v, True)) < 2e-2
 
 
-@pytest.mark.parametrize("V", [50304, 32000, 1000])
+@pytest.mark.parametrize("V", [50304, 32000, 1000, 128256])
 def test_linear_cross_entropy(V):
     torch.manual_seed(0)
     N, C = 512, 256
@@ -317,3 +317,47 @@ def test_llama_trainer_step_gpu():
     for _ in range(5):
         l1 = float(tr.step([(x, x)]))
     assert l1 == l1 and l1 < l0
+
+
+@pytest.mark.parametrize("shape", [(32768, 768, 768), (16384, 2304, 768), (8192, 512, 1024)])
+def test_wgrad_split_k(shape):
+    """split-K weight gradient (batched GEMM over token chunks + HIP slab_sum) vs fp32."""
+    from orion_amd.ops.gemm import wgrad, wgrad_splits
+    M, n1, n2 = shape
+    torch.manual_seed(0)
+    dy, x = bf(M, n1), bf(M, n2)
+    ref_w = dy.float().t() @ x.float()
+    s = torch.tensor([0.25], device=DEV)
+    assert wgrad_splits(M, n1, n2) > 1
+    assert rel_err(wgrad(dy, x), ref_w) < 8e-3
+    assert rel_err(wgrad(dy, x, s), 0.25 * ref_w) < 8e-3
+
+
+def test_slab_sum_order_and_scale():
+    torch.manual_seed(0)
+    slabs = torch.randn(7, 33, 64, device=DEV)
+    s = torch.tensor([-1.5], device=DEV)
+    from orion_amd.ops._ext import C
+    out = C().slab_sum(slabs, s)
+    assert out.dtype == torch.bfloat16 and out.shape == (33, 64)
+    assert rel_err(out, -1.5 * slabs.sum(0)) < 5e-3
+    assert torch.equal(C().slab_sum(slabs, s), out)  # deterministic
+
+
+def test_xent_ignore_index_and_unaligned_targets():
+    """count_valid's vector path needs 16-byte aligned targets; an offset view takes the
+    scalar path.  Rows with ignore_index get zero loss and zero gradient."""
+    torch.manual_seed(0)
+    N, V, C = 515, 1000, 64
+    x = bf(N, C).requires_grad_()
+    w = bf(V, C, scale=0.1).requires_grad_()
+    tall = torch.randint(0, V, (N + 1,), device=DEV)
+    t = tall[1:]  # 8-byte offset: not 16-byte aligned
+    t[::3] = -1
+    loss = ops.linear_cross_entropy(x, w, t, ignore_index=-1)
+    loss.backward()
+    xr, wr = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    lr_ = torch.nn.functional.cross_entropy(xr @ wr.t(), t, ignore_index=-1)
+    lr_.backward()
+    assert abs(loss.item() - lr_.item()) < 2e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2 and rel_err(w.grad, wr.grad) < 2e-2
