@@ -38,75 +38,11 @@
 // conflict-free on the 64-bank LDS.
 #include "common.h"
 #include "attn_params.h"
+#include "mfma_lds.h"
 
 namespace orion {
 
 
-
-template <int D>
-ORION_DEVICE int swz(int r) {
-  if constexpr (D == 128) {
-    return ((r & 3) << 2) | ((r >> 2) & 3);
-  } else {
-    return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1) | ((r >> 2) & 1);
-  }
-}
-
-// element offset of (row, col) in a swizzled [rows][D] bf16 image
-template <int D>
-ORION_DEVICE int loff(int row, int col) {
-  return row * D + ((((col >> 3) ^ swz<D>(row))) << 3) + (col & 7);
-}
-
-ORION_DEVICE bf16x8 lds_b128(const bf16_t* base, int off) {
-  return *reinterpret_cast<const bf16x8*>(base + off);
-}
-
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-
-ORION_DEVICE bf16x4 lds_tr(const bf16_t* base, int off) {
-  typedef __attribute__((address_space(3))) s16x4 lds_s4;
-  s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
-  return __builtin_bit_cast(bf16x4, r);
-}
-
-ORION_DEVICE bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
-
-ORION_DEVICE f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_mfma, a),
-                                                 __builtin_bit_cast(bf16x8_mfma, b), c, 0, 0, 0);
-}
-
-ORION_DEVICE f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
-
-// 16 fp32 accumulator registers rr = 8s..8s+7 -> one bf16 MFMA fragment
-ORION_DEVICE bf16x8 acc_to_frag(const f32x16& x, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = f2bf(x[8 * s + j]);
-  return r;
-}
-
-// Transposed 8-element fragment of a swizzled [rows][D] image:
-// element j of lane (group g = lane>>4, i = lane&15) is image[row0 + 8*(j>>2) + (j&3)][col]
-// with row0 = rbase + (i>>2) supplied per lane and col = cbase + 16*(g&1) + 4*(i&3).
-template <int D>
-ORION_DEVICE bf16x8 tr_frag(const bf16_t* img, int rbase, int cbase, int lane, int rstep) {
-  const int g = lane >> 4, i = lane & 15;
-  const int row = rbase + (i >> 2);
-  const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
-  return cat8(lds_tr(img, loff<D>(row, col)), lds_tr(img, loff<D>(row + rstep, col)));
-}
 
 // ============================================================================ forward
 template <int D, bool CAUSAL>
@@ -298,7 +234,8 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
   bf16_t* St = Ds + 2 * QT;                // [4 waves][32 keys][32 q]
   float* lse_s = reinterpret_cast<float*>(St + 4 * 32 * 32);  // [2][32]
   float* del_s = lse_s + 64;                                  // [2][32]
-  float* dqr = del_s + 64;                                    // [4][32][D]
+  constexpr int DQP = BMQ + 4;  // padded q-row of the [d][q] dQ partials (conflict-free b128)
+  float* dqr = del_s + 64;                                    // [4][D][DQP]
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h32 = lane >> 5, l32 = lane & 31;
@@ -379,7 +316,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
   };
 
   bf16_t* Sw = St + wv * 32 * 32;
-  float* dqw = dqr + wv * 32 * D;
+  float* dqw = dqr + wv * D * DQP;
   const int mykey = kw0 + l32;
 
   if (total > 0) {
@@ -420,7 +357,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
             if (mykey >= p.Tk || q >= p.T || (CAUSAL && mykey > q + off)) pv = 0.f;
           }
           s[r] = pv;
-          dp[r] = pv * (dp[r] - Dl[j]) * p.scale;
+          dp[r] = pv * (dp[r] - Dl[j]);  // dS / scale: the scale is applied to dK and dQ once
         }
       }
       bf16x8 pb[2], sb[2];
@@ -436,12 +373,12 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
           dka[db] = mfma32(tr_frag<D>(Qc, 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
         }
       // dS^T image [key][q] (64-byte rows, unswizzled: the transposed read of 4 rows x 32
-      // columns covers all 64 banks exactly once)
+      // columns covers all 64 banks exactly once); the bf16 values are the sb fragments
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         bf16x4 v4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = f2bf(dp[4 * g4 + j]);
+        for (int j = 0; j < 4; ++j) v4[j] = sb[g4 >> 1][4 * (g4 & 1) + j];
         *reinterpret_cast<bf16x4*>(Sw + l32 * 32 + 8 * g4 + 4 * h32) = v4;
       }
       // dQ partial = dS K over this wave's 32 keys (A and B both by transposed reads)
@@ -465,24 +402,38 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) dq[db] = zero16();
     }
-    // per-wave dQ partial -> LDS [q][d]
+    // per-wave dQ partial -> LDS as [d][q] (rows of DQP floats): accumulator registers
+    // 4g..4g+3 are 4 consecutive q of one d, so each goes out as ONE 16-byte write
 #pragma unroll
     for (int db = 0; db < D / 32; ++db)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = (r & 3) + 8 * (r >> 2) + 4 * h32;
-        dqw[q * D + db * 32 + l32] = dq[db][r];
+      for (int g4 = 0; g4 < 4; ++g4) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = dq[db][4 * g4 + j];
+        *reinterpret_cast<f32x4*>(dqw + (db * 32 + l32) * DQP + 8 * g4 + 4 * h32) = v;
       }
     if (it + 1 < total) swrite(buf ^ 1);
     __syncthreads();
-    // fold the 4 waves and add to the fp32 dQ accumulator (256-byte rows per wave instr)
+    // fold the 4 waves (16-byte reads of 4 q's) and add scale * sum to the fp32 dQ
+    // accumulator: lanes run over d, so each atomic instruction covers D contiguous floats
     {
       float* dqg = p.dq_acc + (((long)b * p.Hq + hq) * p.T) * D;
 #pragma unroll
-      for (int e = tid; e < BMQ * D; e += 256) {
-        const int q = e / D;
-        const float sum = dqr[e] + dqr[BMQ * D + e] + dqr[2 * BMQ * D + e] + dqr[3 * BMQ * D + e];
-        if (qbase + q < p.T && !(p.flags & 1)) atomicAdd(dqg + (long)(qbase + q) * D + (e % D), sum);
+      for (int k = 0; k < D / 32; ++k) {
+        const int e = tid + k * 256;
+        const int d = e % D, qg = e / D;
+        const int o = d * DQP + 4 * qg;
+        f32x4 sum = *reinterpret_cast<const f32x4*>(dqr + o);
+#pragma unroll
+        for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const f32x4*>(dqr + w * D * DQP + o);
+        if (!(p.flags & 1)) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int q = qbase + 4 * qg + j;
+            if (q < p.T) atomicAdd(dqg + (long)q * D + d, sum[j] * p.scale);
+          }
+        }
       }
     }
     __syncthreads();
@@ -499,7 +450,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
         bf16x4 k4, v4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          k4[j] = f2bf(dka[db][4 * g4 + j]);
+          k4[j] = f2bf(dka[db][4 * g4 + j] * p.scale);
           v4[j] = f2bf(dva[db][4 * g4 + j]);
         }
         *reinterpret_cast<bf16x4*>(dKb + db * 32 + 8 * g4 + 4 * h32) = k4;
@@ -537,7 +488,7 @@ extern "C++" {
 
 static size_t fwd_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
 static size_t bwd_lds(int D) {
-  return (size_t)128 * D * 2 + 4 * 32 * D * 2 + 4 * 32 * 32 * 2 + 128 * 4 + 4 * 32 * D * 4;
+  return (size_t)128 * D * 2 + 4 * 32 * D * 2 + 4 * 32 * 32 * 2 + 128 * 4 + 4 * D * (32 + 4) * 4;
 }
 
 template <int D, bool CAUSAL>

@@ -30,6 +30,10 @@ int orion_swiglu_fwd(const void*, void*, long, int, hipStream_t);
 int orion_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_scale_bf16(void*, const float*, long, hipStream_t);
 int orion_slab_sum(const float*, int, long, void*, const float*, hipStream_t);
+int orion_wgrad_splits(int, int, int);
+int orion_wgrad_effective_splits(int, int);
+int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
+                const float*, hipStream_t);
 int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
 int orion_sumsq_partials();
 int orion_grad_sumsq(const void*, long, float*, float*, hipStream_t);
@@ -288,6 +292,36 @@ Tensor slab_sum(const Tensor& slabs, const c10::optional<Tensor>& scale) {
   return out;
 }
 
+// dW = dy^T x over the token dim (csrc/wgrad.hip); splits = 0 picks the split-K count
+Tensor wgrad(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& scale, int64_t splits) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad: dy (M,N1), x (M,N2)");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad: rows must be contiguous");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  const int M = dy.size(0), N1 = dy.size(1), N2 = x.size(1);
+  int S = splits > 0 ? orion_wgrad_effective_splits(M, (int)splits) : orion_wgrad_splits(M, N1, N2);
+  const float* sc = nullptr;
+  if (scale.has_value() && scale->defined()) {
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "scale must be one fp32");
+    sc = scale->data_ptr<float>();
+  }
+  auto out = at::empty({N1, N2}, dy.options());
+  if (S > 1) {
+    auto slabs = at::empty({S, N1, N2}, dy.options().dtype(at::kFloat));
+    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, S,
+                             slabs.data_ptr<float>(), nullptr, nullptr, cur_stream()), "wgrad");
+    check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc,
+                                cur_stream()), "wgrad slab_sum");
+  } else {
+    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, 1,
+                             nullptr, out.data_ptr(), sc, cur_stream()), "wgrad");
+  }
+  return out;
+}
+
+int64_t wgrad_splits(int64_t M, int64_t N1, int64_t N2) { return orion_wgrad_splits(M, N1, N2); }
+
 // ------------------------------------------------------------------ optimizer
 void grad_sumsq(const Tensor& g, Tensor out) {
   check_bf16(g, "grads");
@@ -483,6 +517,8 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("swiglu_bwd(Tensor dy, Tensor gu) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("slab_sum(Tensor slabs, Tensor? scale=None) -> Tensor");
+  m.def("wgrad(Tensor dy, Tensor x, Tensor? scale=None, int splits=0) -> Tensor");
+  m.def("wgrad_splits(int M, int N1, int N2) -> int", &wgrad_splits);  // host-only helper
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
@@ -505,6 +541,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("scale_", &scale_);
   m.impl("slab_sum", &slab_sum);
+  m.impl("wgrad", &wgrad);
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
   m.impl("grad_sumsq", &grad_sumsq);
   m.impl("adamw_flat", &adamw_flat);

@@ -1,4 +1,9 @@
-"""Weight-gradient GEMM with explicit split-K over the token dimension.
+"""Weight-gradient GEMM dW = dY^T X (reduction over the token dimension).
+
+Default path: the hand-written MFMA kernel of ``csrc/wgrad.hip`` (k-major operands
+through transposed LDS reads, split-K into fp32 slabs, XCD-aware tiles).  The
+``ORION_WGRAD=bmm`` path below is the library alternative it replaced, kept for
+A/B measurement:
 
 dW = dY^T X reduces over all B*T tokens (65,536 rows for the GPT-2 bench) into
 a small output (768 x 768 ... 3072 x 768).  A single GEMM of that shape has only
@@ -22,6 +27,14 @@ import torch
 from ._ext import C
 
 _FORCE = os.environ.get("ORION_WGRAD_SPLITS")
+_IMPL = os.environ.get("ORION_WGRAD", "bmm")  # "hip" (csrc/wgrad.hip) | "bmm"
+
+
+def _hip_ok(dy, x):
+    return (_IMPL == "hip" and dy.is_cuda and dy.shape[0] % 32 == 0 and dy.shape[1] % 8 == 0
+            and x.shape[1] % 8 == 0 and dy.stride(1) == 1 and x.stride(1) == 1
+            and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0
+            and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
 def wgrad_splits(M: int, n1: int, n2: int) -> int:
@@ -40,6 +53,8 @@ def wgrad_splits(M: int, n1: int, n2: int) -> int:
 
 def wgrad(dy: torch.Tensor, x: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Tensor:
     """dy (M, n1), x (M, n2) bf16 -> dy^T x (n1, n2) bf16 [times the device scalar ``scale``]."""
+    if _hip_ok(dy, x):
+        return C().wgrad(dy, x, scale, int(_FORCE or 0))
     M, n1 = dy.shape
     n2 = x.shape[1]
     S = wgrad_splits(M, n1, n2)

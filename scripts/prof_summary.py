@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Condense a rocprofv3 kernel_stats.csv: per-step ms per kernel (short names) and per category.
+
+usage: python scripts/prof_summary.py gpurun_out/prof/run_kernel_stats.csv --steps 5
+"""
+import argparse
+import csv
+import re
+
+
+def short(name):
+    if name.startswith(("Cijk_", "Custom_Cijk")):
+        m = re.search(r"MT(\d+x\d+x\d+)", name)
+        lay = re.search(r"Cijk_(A\w\w\w_B\w\w\w)", name)
+        return f"gemm[{lay.group(1) if lay else '?'} {m.group(1) if m else '?'}]"
+    name = re.sub(r"\(.*", "", name)
+    name = re.sub(r"^void ", "", name)
+    name = name.replace("orion::", "")
+    name = re.sub(r"at::native::(\(anonymous namespace\)::)?", "at::", name)
+    return name[:70]
+
+
+def category(s):
+    if s.startswith("gemm"):
+        return "gemm"
+    for k in ("attn", "xent", "ln_", "gelu", "colsum", "slab_sum", "adamw", "sumsq", "rms", "rope", "swiglu"):
+        if k in s:
+            return k.strip("_")
+    return "other"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--top", type=int, default=30)
+    a = ap.parse_args()
+    rows = []
+    with open(a.csv) as f:
+        for r in csv.DictReader(f):
+            rows.append((short(r["Name"]), int(r["Calls"]), float(r["TotalDurationNs"]) / 1e6))
+    agg = {}
+    for n, c, t in rows:
+        k = agg.setdefault(n, [0, 0.0])
+        k[0] += c
+        k[1] += t
+    tot = sum(v[1] for v in agg.values())
+    print(f"total {tot / a.steps:.2f} ms/step over {a.steps} steps")
+    print(f"{'kernel':72s} {'calls/st':>8s} {'ms/step':>8s} {'%':>6s}")
+    for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        print(f"{n:72s} {c / a.steps:8.1f} {t / a.steps:8.3f} {100 * t / tot:6.2f}")
+    cats = {}
+    for n, (c, t) in agg.items():
+        cats[category(n)] = cats.get(category(n), 0.0) + t
+    print("\nby category (ms/step):", ", ".join(f"{k}={v / a.steps:.2f}" for k, v in sorted(cats.items(), key=lambda kv: -kv[1])))
+
+
+if __name__ == "__main__":
+    main()

@@ -92,3 +92,27 @@ def test_broken_trials_stop_worker(tmp_path):
     store = Database("sqlite", host=db)
     (exp,) = store.read("experiments", {"name": "broken"})
     assert store.count("trials", {"experiment": exp["_id"], "status": "broken"}) == 3
+
+
+def test_orion_tunes_train_py(tmp_path):
+    """SURVEY.md §7.4's end-to-end slice on CPU: the orion CLI searches the trainer's
+    learning rate; every trial trains GPT-2-tiny and reports its val loss."""
+    db = str(tmp_path / "orion.sqlite")
+    out = tmp_path / "out"
+    rc = subprocess.call(ORION + ["-n", "lr_sweep", "--max-trials", "2", "--pool-size", "1",
+                                  os.path.join(ROOT, "train.py"), "--device=cpu", "--model=gpt2-tiny",
+                                  "--n_layer=1", "--n_head=2", "--n_embd=64", "--block_size=16",
+                                  "--batch_size=2", "--gradient_accumulation_steps=1", "--max_iters=2",
+                                  "--eval_interval=2", "--eval_iters=1", f"--out_dir={out}", "--dataset=",
+                                  "--learning_rate~loguniform(1e-4, 1e-2)"],
+                         cwd=str(tmp_path), env=_env(db), timeout=600)
+    assert rc == 0
+    store = Database("sqlite", host=db)
+    (exp,) = store.read("experiments", {"name": "lr_sweep"})
+    trials = store.read("trials", {"experiment": exp["_id"]})
+    assert len(trials) >= 2 and all(t["status"] == "completed" for t in trials)
+    for t in trials:
+        (p,) = t["params"]
+        assert p["name"] == "/learning_rate" and 1e-4 <= p["value"] < 1e-2
+        (r,) = [r for r in t["results"] if r["type"] == "objective"]
+        assert r["name"] == "val_loss" and r["value"] > 0

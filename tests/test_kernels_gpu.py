@@ -319,18 +319,43 @@ def test_llama_trainer_step_gpu():
     assert l1 == l1 and l1 < l0
 
 
-@pytest.mark.parametrize("shape", [(32768, 768, 768), (16384, 2304, 768), (8192, 512, 1024)])
-def test_wgrad_split_k(shape):
-    """split-K weight gradient (batched GEMM over token chunks + HIP slab_sum) vs fp32."""
-    from orion_amd.ops.gemm import wgrad, wgrad_splits
+@pytest.mark.parametrize("shape", [(32768, 768, 768), (16384, 2304, 768), (8192, 512, 1024),
+                                   (4096, 1000, 264), (65536, 768, 3072), (2048, 50304, 768)])
+@pytest.mark.parametrize("splits", [0, 1, 5])
+def test_wgrad_kernel(shape, splits):
+    """csrc/wgrad.hip (transposed-LDS MFMA, split-K slabs) vs fp32, incl. ragged N1/N2."""
+    from orion_amd.ops._ext import C
     M, n1, n2 = shape
     torch.manual_seed(0)
     dy, x = bf(M, n1), bf(M, n2)
     ref_w = dy.float().t() @ x.float()
     s = torch.tensor([0.25], device=DEV)
-    assert wgrad_splits(M, n1, n2) > 1
-    assert rel_err(wgrad(dy, x), ref_w) < 8e-3
-    assert rel_err(wgrad(dy, x, s), 0.25 * ref_w) < 8e-3
+    out = C().wgrad(dy, x, None, splits)
+    assert out.shape == (n1, n2) and out.dtype == torch.bfloat16
+    assert rel_err(out, ref_w) < 8e-3
+    assert rel_err(C().wgrad(dy, x, s, splits), 0.25 * ref_w) < 8e-3
+
+
+def test_wgrad_strided_rows():
+    """row stride != width (a column slice of a wider activation)."""
+    from orion_amd.ops._ext import C
+    torch.manual_seed(0)
+    big = bf(4096, 1024)
+    dy, x = big[:, :512], bf(4096, 256)
+    assert rel_err(C().wgrad(dy, x, None, 0), dy.float().t() @ x.float()) < 8e-3
+
+
+@pytest.mark.parametrize("shape", [(32768, 768, 768), (16384, 2304, 768)])
+def test_wgrad_bmm_split_k(shape, monkeypatch):
+    """library alternative: batched GEMM over token chunks + HIP slab_sum."""
+    from orion_amd.ops import gemm
+    monkeypatch.setattr(gemm, "_IMPL", "bmm")
+    M, n1, n2 = shape
+    torch.manual_seed(0)
+    dy, x = bf(M, n1), bf(M, n2)
+    ref_w = dy.float().t() @ x.float()
+    assert gemm.wgrad_splits(M, n1, n2) > 1
+    assert rel_err(gemm.wgrad(dy, x), ref_w) < 8e-3
 
 
 def test_slab_sum_order_and_scale():
