@@ -276,6 +276,52 @@ __global__ __launch_bounds__(256) void colsum_stage2_kernel(const float* __restr
 
 constexpr int COLSUM_SPLITS = 16;
 
+// The LN backward's three column sums (dgamma, dbeta, branch-bias grad) in one launch
+// pair: blockIdx.z picks the [P][C] partial matrix part + z*P*C; z whose output is
+// null is skipped (block-uniform exit, before any barrier).
+struct ColsumOuts {
+  bf16_t* out[3];
+};
+
+__global__ __launch_bounds__(256) void colsum3_stage1_kernel(const float* __restrict__ part,
+                                                             float* __restrict__ mid, int P, int C,
+                                                             int rows_per_split, ColsumOuts o) {
+  if (!o.out[blockIdx.z]) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const float* pz = part + (size_t)blockIdx.z * P * C;
+  const int p0 = blockIdx.y * rows_per_split, p1 = min(P, p0 + rows_per_split);
+  float s = 0.f;
+  if (c < C) {
+    int p = p0 + wv;
+    for (; p + 28 < p1; p += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pz[(size_t)(p + 4 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; p < p1; p += 4) s += pz[(size_t)p * C + c];
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && c < C)
+    mid[((size_t)blockIdx.z * gridDim.y + blockIdx.y) * C + c] =
+        red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
+__global__ __launch_bounds__(256) void colsum3_stage2_kernel(const float* __restrict__ mid, int S,
+                                                             int C, ColsumOuts o) {
+  bf16_t* out = o.out[blockIdx.y];
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (!out || c >= C) return;
+  const float* mz = mid + (size_t)blockIdx.y * S * C;
+  float s = 0.f;
+  for (int i = 0; i < S; ++i) s += mz[(size_t)i * C + c];
+  out[c] = f2bf(s);
+}
+
 }  // namespace orion
 
 using namespace orion;
@@ -367,9 +413,12 @@ int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const floa
     }
   }
   float* mid = part + 3 * (size_t)nb * C;
-  if (dw) orion_colsum_partials2(pdw, mid, dw, nb, C, st);
-  if (db) orion_colsum_partials2(pdb, mid + (size_t)COLSUM_SPLITS * C, db, nb, C, st);
-  if (drbias) orion_colsum_partials2(pdx, mid + 2 * (size_t)COLSUM_SPLITS * C, drbias, nb, C, st);
+  if (dw || db || drbias) {
+    const ColsumOuts o{{(bf16_t*)dw, (bf16_t*)db, (bf16_t*)drbias}};
+    const int rps = (nb + COLSUM_SPLITS - 1) / COLSUM_SPLITS;
+    colsum3_stage1_kernel<<<dim3((C + 63) / 64, COLSUM_SPLITS, 3), 256, 0, st>>>(part, mid, nb, C, rps, o);
+    colsum3_stage2_kernel<<<dim3((C + 255) / 256, 3), 256, 0, st>>>(mid, COLSUM_SPLITS, C, o);
+  }
   return (int)hipGetLastError();
 }
 

@@ -23,11 +23,6 @@
 
 namespace orion {
 
-constexpr int WG_T = 512;          // 8 waves: 2 along n1 x 4 along n2
-constexpr int WG_BK = 32;          // m rows per stage
-constexpr int WG_NS = 4;           // LDS ring depth (3 stages in flight during compute)
-constexpr int IMG = WG_BK * 128;   // one [32][128] bf16 image (8 KB)
-constexpr int WG_STAGE = 4 * IMG;  // A halves 0,1 | B halves 0,1 = 32 KB
 
 ORION_DEVICE void glds16(const bf16_t* g, bf16_t* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -36,7 +31,7 @@ ORION_DEVICE void glds16(const bf16_t* g, bf16_t* l) {
 
 // ds_read_b64_tr_b16 as inline asm: LDS reads the compiler cannot see, so its waitcnt
 // pass does not drain the in-flight LDS-DMA ring (vmcnt(0)) before them (the builtin
-// form gets exactly that).  Completion is waited for by hand: lds_wait() below.
+// form gets exactly that).  Completion is waited for by hand (lgkmcnt, below).
 ORION_DEVICE bf16x4 tr_read(const bf16_t* lds, int elem) {
   const unsigned addr =
       (unsigned)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(lds + elem));
@@ -45,7 +40,7 @@ ORION_DEVICE bf16x4 tr_read(const bf16_t* lds, int elem) {
   return r;
 }
 
-// tr_frag (mfma_lds.h) on the asm read
+// tr_frag (mfma_lds.h) on the asm read, [rows][128] image, rows r and r + 8
 ORION_DEVICE bf16x8 tr_frag_asm(const bf16_t* img, int rbase, int cbase, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = rbase + (i >> 2);
@@ -53,23 +48,50 @@ ORION_DEVICE bf16x8 tr_frag_asm(const bf16_t* img, int rbase, int cbase, int lan
   return cat8(tr_read(img, loff<128>(row, col)), tr_read(img, loff<128>(row + 8, col)));
 }
 
-ORION_DEVICE void wait_vm(int n) {  // retire all but the newest n vector-memory ops of this wave
-  if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// wait until at most N LDS reads are outstanding; the fragments are "+v" operands so
+// no MFMA reading them can be scheduled before the wait
+template <int N, int TA>
+ORION_DEVICE void lds_wait_frags(bf16x8 (&af)[TA], bf16x8 (&bf)[2]) {
+  if constexpr (TA == 4) {
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bf[0]), "+v"(bf[1])
+                 : "n"(N));
+  } else if constexpr (TA == 2) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(af[0]), "+v"(af[1]), "+v"(bf[0]), "+v"(bf[1]) : "n"(N));
+  } else {
+    static_assert(TA == 1, "TA in {1, 2, 4}");
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(af[0]), "+v"(bf[0]), "+v"(bf[1]) : "n"(N));
+  }
 }
 
-// Staging is LDS-DMA (global_load_lds_dwordx4): no VGPRs, so a 4-deep ring keeps
-// ~96 KB per CU in flight -- the register-staged versions (32-48 KB in flight)
-// ran latency-bound at ~0.8 PF/s.  A wave-instruction writes 1 KB lane-linearly
-// (4 rows of one 128-column image); the XOR swizzle of the image is applied to the
-// per-lane SOURCE column instead.  Barriers are raw s_barrier with counted vmcnt
-// (a __syncthreads() would drain every in-flight stage).
-__global__ __launch_bounds__(WG_T) void wgrad_kernel(
+template <int N>
+ORION_DEVICE void wait_vm_exact() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Staging is LDS-DMA (global_load_lds_dwordx4): no VGPRs, so a ring of NS stages
+// keeps NS-1 stages per CU in flight (register staging held 32-48 KB and ran
+// latency-bound at ~0.8 PF/s).  A wave-instruction writes 1 KB lane-linearly (4
+// rows of one 128-column image); the image's XOR swizzle is applied to the per-lane
+// SOURCE column instead.  Barriers are raw s_barrier with counted vmcnt (a
+// __syncthreads() would drain every in-flight stage).  Inside a stage the fragment
+// reads of k16 step s+1 are issued before the MFMAs of step s (sched_barrier keeps
+// the compiler from regrouping them).
+// KS k16 steps (16 rows each) per stage, NS-deep ring, WM waves along n1 (each owning
+// 256/WM rows = TA MFMA tiles) x 4 waves along n2 (64 columns each)
+template <int KS, int NS, int WM>
+__global__ __launch_bounds__(WM * 256) void wgrad_kernel(
     const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B, long ldb, int M, int N1,
     int N2, int tiles_n2, int ntiles, int chunk, float* __restrict__ slabs,
     bf16_t* __restrict__ out, const float* __restrict__ scale) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [WG_NS stages][A0 A1 B0 B1]
+  constexpr int BK = 16 * KS;        // m rows per stage
+  constexpr int IMG = BK * 128;      // one [BK][128] image
+  constexpr int STAGE = 4 * IMG;     // A halves 0,1 | B halves 0,1
+  constexpr int NW = WM * 4;          // waves
+  constexpr int TA = 8 / WM;          // 32-row MFMA tiles per wave along n1
+  constexpr int BPW = KS * 8 / NW;    // 1-KB blocks per wave per operand per stage
+  static_assert(BPW * NW == KS * 8, "stage blocks must divide over the waves");
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h32 = lane >> 5;
   const int wr = wv >> 2, wc = wv & 3;
@@ -81,70 +103,90 @@ __global__ __launch_bounds__(WG_T) void wgrad_kernel(
   const int kc = wid / ntiles, tile = wid % ntiles;
   const int n10 = (tile / tiles_n2) * 256, n20 = (tile % tiles_n2) * 256;
   const int m0 = kc * chunk;
-  const int nsteps = (min(M, m0 + chunk) - m0) / WG_BK;
+  const int nsteps = (min(M, m0 + chunk) - m0) / BK;
 
-  // this wave's two 1-KB blocks of each operand per stage: block blk covers image half
-  // blk>>3, rows 4*(blk&7)..+3; lane -> row +lane/16, LDS slot lane%16 = source chunk ^ swz
-  long goffA[2], goffB[2];
-  int loffs[2];
+  // block blk (0 .. 8*KS-1) of an operand: image half blk / (4*KS), rows 4*(blk % (4*KS))..+3;
+  // lane -> row + lane/16, LDS slot lane%16 = source chunk ^ swz(row)
+  long goffA[BPW], goffB[BPW];
+  int loffs[BPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int blk = wv * 2 + i, half = blk >> 3;
-    const int row = 4 * (blk & 7) + (lane >> 4), slot = lane & 15;
+  for (int i = 0; i < BPW; ++i) {
+    const int blk = wv * BPW + i, half = blk / (4 * KS), rb4 = blk % (4 * KS);
+    const int row = 4 * rb4 + (lane >> 4), slot = lane & 15;
     const int col = half * 128 + 8 * (slot ^ swz<128>(row));
     goffA[i] = (long)row * lda + min(n10 + col, N1 - 8);
     goffB[i] = (long)row * ldb + min(n20 + col, N2 - 8);
-    loffs[i] = half * IMG + (blk & 7) * 512;
+    loffs[i] = half * IMG + rb4 * 512;
   }
   auto issue = [&](int step) {
-    bf16_t* base = smem + (step % WG_NS) * WG_STAGE;
-    const long mr = m0 + (long)step * WG_BK;
+    bf16_t* base = smem + (step % NS) * STAGE;
+    const long mr = m0 + (long)step * BK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < BPW; ++i) {
       glds16(A + mr * lda + goffA[i], base + loffs[i]);
       glds16(B + mr * ldb + goffB[i], base + 2 * IMG + loffs[i]);
     }
   };
 
-  f32x16 acc[4][2];
+  f32x16 acc[TA][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < TA; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
 
-  const int pre = min(nsteps, WG_NS - 1);
+  const int pre = min(nsteps, NS - 1);
   for (int st = 0; st < pre; ++st) issue(st);
   for (int t = 0; t < nsteps; ++t) {
-    wait_vm(4 * min(nsteps - 1 - t, WG_NS - 2));  // this wave's share of stage t has landed
-    asm volatile("s_barrier" ::: "memory");        // ... and every other wave's; stage t-1 is free
-    if (t + WG_NS - 1 < nsteps) issue(t + WG_NS - 1);  // refill the slot stage t-1 used
-    const bf16_t* As = smem + (t % WG_NS) * WG_STAGE + wr * IMG;
-    const bf16_t* Bs = smem + (t % WG_NS) * WG_STAGE + 2 * IMG + (wc >> 1) * IMG;
-    // both k16 steps' fragments are requested up front (24 reads); the first step's
-    // MFMAs start once its 12 reads have returned (lgkmcnt counts in issue order)
-    bf16x8 af[2][4], bfr[2][2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) af[s][a] = tr_frag_asm(As, 16 * s + 4 * h32, a * 32, lane);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) bfr[s][b] = tr_frag_asm(Bs, 16 * s + 4 * h32, (wc & 1) * 64 + b * 32, lane);
+    // this wave's share of stage t has landed (stages t+1 .. t+NS-2 may stay in flight)
+    const int ahead = min(nsteps - 1 - t, NS - 2);
+    constexpr int PS = 2 * BPW;  // glds instructions per stage per wave
+    if constexpr (NS >= 8) {
+      if (ahead >= 6) wait_vm_exact<6 * PS>();
+      else if (ahead == 5) wait_vm_exact<5 * PS>();
+      else if (ahead == 4) wait_vm_exact<4 * PS>();
+      else if (ahead == 3) wait_vm_exact<3 * PS>();
+      else if (ahead == 2) wait_vm_exact<2 * PS>();
+      else if (ahead == 1) wait_vm_exact<PS>();
+      else wait_vm_exact<0>();
+    } else if constexpr (NS >= 4) {
+      if (ahead >= 2) wait_vm_exact<2 * PS>();
+      else if (ahead == 1) wait_vm_exact<PS>();
+      else wait_vm_exact<0>();
+    } else if constexpr (NS == 3) {
+      if (ahead >= 1) wait_vm_exact<PS>();
+      else wait_vm_exact<0>();
+    } else {
+      wait_vm_exact<0>();
     }
-    // the "+v" operands pin every MFMA that reads a fragment after its wait
-    asm volatile("s_waitcnt lgkmcnt(12)"
-                 : "+v"(af[0][0]), "+v"(af[0][1]), "+v"(af[0][2]), "+v"(af[0][3]), "+v"(bfr[0][0]),
-                   "+v"(bfr[0][1]));
+    asm volatile("s_barrier" ::: "memory");  // every wave's share landed; slot of stage t-1 free
+    if (t + NS - 1 < nsteps) issue(t + NS - 1);
+    const bf16_t* As = smem + (t % NS) * STAGE + (wr * TA * 32 / 128) * IMG;
+    const bf16_t* Bs = smem + (t % NS) * STAGE + 2 * IMG + (wc >> 1) * IMG;
+    bf16x8 af[2][TA], bfr[2][2];
+    auto fetch = [&](int s, int slot) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < TA; ++a)
+        af[slot][a] = tr_frag_asm(As, 16 * s + 4 * h32, (wr * TA * 32) % 128 + a * 32, lane);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[0][a], bfr[0][b], acc[a][b]);
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(af[1][0]), "+v"(af[1][1]), "+v"(af[1][2]), "+v"(af[1][3]), "+v"(bfr[1][0]),
-                   "+v"(bfr[1][1]));
+      for (int b = 0; b < 2; ++b)
+        bfr[slot][b] = tr_frag_asm(Bs, 16 * s + 4 * h32, (wc & 1) * 64 + b * 32, lane);
+    };
+    fetch(0, 0);
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int s = 0; s < KS; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < KS) {
+        fetch(s + 1, cur ^ 1);
+        lds_wait_frags<2 * (TA + 2), TA>(af[cur], bfr[cur]);  // step s = the older half
+      } else {
+        lds_wait_frags<0, TA>(af[cur], bfr[cur]);
+      }
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[1][a], bfr[1][b], acc[a][b]);
+      for (int a = 0; a < TA; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[cur][a], bfr[cur][b], acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -153,13 +195,13 @@ __global__ __launch_bounds__(WG_T) void wgrad_kernel(
   const float sc = (!slabs && scale) ? *scale : 1.f;
   float* sl = slabs ? slabs + (long)kc * N1 * N2 : nullptr;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < TA; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int n2 = n20 + wc * 64 + b * 32 + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int n1 = n10 + wr * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+        const int n1 = n10 + wr * TA * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
         if (n1 < N1 && n2 < N2) {
           if (sl) sl[(long)n1 * N2 + n2] = acc[a][b][r];
           else out[(long)n1 * N2 + n2] = f2bf(acc[a][b][r] * sc);
@@ -168,9 +210,25 @@ __global__ __launch_bounds__(WG_T) void wgrad_kernel(
     }
 }
 
+// kernel configurations: {KS, NS}; LDS = NS * KS * 32 KB <= 160 KB
+struct WgCfg { int ks, ns, wm; };
+constexpr WgCfg WG_CFGS[] = {{2, 4, 4}, {2, 4, 2}, {4, 2, 2}, {2, 2, 4}};
+
+static int wg_cfg() {
+  static int c = -1;
+  if (c < 0) {
+    const char* e = getenv("ORION_WGRAD_CFG");
+    c = e ? atoi(e) : 0;
+    if (c < 0 || c > 3) c = 0;
+  }
+  return c;
+}
+
 }  // namespace orion
 
 using namespace orion;
+
+static int wg_bk() { return 16 * WG_CFGS[wg_cfg()].ks; }
 
 // Split count: minimise (rounds of one-workgroup-per-CU) x (rows per workgroup) plus
 // the fp32 slab round trip, in units of rows of work.
@@ -180,8 +238,9 @@ int orion_wgrad_splits(int M, int N1, int N2) {
   double best = 1e30;
   int bestS = 1;
   for (int S = 1; S <= 32; ++S) {
-    const int chunk = ((M / WG_BK + S - 1) / S) * WG_BK;
-    if (chunk < 8 * WG_BK && S > 1) break;
+    const int BK = wg_bk();
+    const int chunk = ((M / BK + S - 1) / S) * BK;
+    if (chunk < 8 * BK && S > 1) break;
     const int Se = (M + chunk - 1) / chunk;
     if (Se != S) continue;
     const long rounds = (tiles * Se + 255) / 256;  // one workgroup per CU (128 KB LDS)
@@ -198,33 +257,52 @@ int orion_wgrad_splits(int M, int N1, int N2) {
 // number of k-chunks actually produced when S are requested (chunks are whole stages)
 int orion_wgrad_effective_splits(int M, int S) {
   if (S < 1) S = 1;
-  const int chunk = ((M / WG_BK + S - 1) / S) * WG_BK;
+  const int BK = wg_bk();
+  const int chunk = ((M / BK + S - 1) / S) * BK;
   return chunk > 0 ? (M + chunk - 1) / chunk : 1;
 }
 
-int orion_wgrad_lds() { return WG_NS * WG_STAGE * (int)sizeof(bf16_t); }
+int orion_wgrad_lds() {
+  const WgCfg c = WG_CFGS[wg_cfg()];
+  return c.ns * c.ks * 16 * 128 * 4 * (int)sizeof(bf16_t);
+}
 
 // A (M x N1, ld lda), B (M x N2, ld ldb) bf16 -> slabs (S, N1, N2) fp32 when S > 1
 // (caller folds them), else out (N1, N2) bf16 scaled by *scale (nullable).
 int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1, int N2, int S,
                 float* slabs, void* out, const float* scale, hipStream_t st) {
-  if (M % WG_BK || N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || N1 < 8 || N2 < 8) return -1;
+  const int BK = wg_bk();
+  if (M % BK || N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || N1 < 8 || N2 < 8) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -2;
-  const int chunk = ((M / WG_BK + S - 1) / S) * WG_BK;
+  const int chunk = ((M / BK + S - 1) / S) * BK;
   const int Se = (M + chunk - 1) / chunk;
   if (Se != S) return -3;
   if (S > 1 && !slabs) return -4;
   const int t1 = (N1 + 255) / 256, t2 = (N2 + 255) / 256;
   const int ntiles = t1 * t2;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            orion_wgrad_lds()) != hipSuccess)
-      return -5;
-    attr = true;
+  const int lds = orion_wgrad_lds();
+  auto Ab = (const bf16_t*)A;
+  auto Bb = (const bf16_t*)B;
+  float* sl = S > 1 ? slabs : nullptr;
+  auto O = (bf16_t*)out;
+#define WG_LAUNCH(KS, NS, WM)                                                                   \
+  {                                                                                             \
+    static bool attr = false;                                                                   \
+    if (!attr) {                                                                                \
+      if (hipFuncSetAttribute((const void*)wgrad_kernel<KS, NS, WM>,                            \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)   \
+        return -5;                                                                              \
+      attr = true;                                                                              \
+    }                                                                                           \
+    wgrad_kernel<KS, NS, WM><<<ntiles * S, WM * 256, lds, st>>>(Ab, lda, Bb, ldb, M, N1, N2, t2, \
+                                                                ntiles, chunk, sl, O, scale);  \
   }
-  wgrad_kernel<<<ntiles * S, WG_T, orion_wgrad_lds(), st>>>(
-      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, M, N1, N2, t2, ntiles, chunk,
-      S > 1 ? slabs : nullptr, (bf16_t*)out, scale);
+  switch (wg_cfg()) {
+    case 0: WG_LAUNCH(2, 4, 4) break;  // measured best on MI355X (16 waves, 122 VGPR)
+    case 1: WG_LAUNCH(2, 4, 2) break;
+    case 2: WG_LAUNCH(4, 2, 2) break;
+    default: WG_LAUNCH(2, 2, 4) break;
+  }
+#undef WG_LAUNCH
   return (int)hipGetLastError();
 }

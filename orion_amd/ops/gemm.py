@@ -27,7 +27,7 @@ import torch
 from ._ext import C
 
 _FORCE = os.environ.get("ORION_WGRAD_SPLITS")
-_IMPL = os.environ.get("ORION_WGRAD", "bmm")  # "hip" (csrc/wgrad.hip) | "bmm"
+_IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/wgrad.hip) | "bmm"
 
 
 def _hip_ok(dy, x):
