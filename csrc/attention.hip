@@ -221,21 +221,30 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnParams p, float* 
 }
 
 // ============================================================================ backward
+// waves (x 32 keys) per backward workgroup.  8 waves (256 keys) halve the dQ atomics
+// but measured 7 % slower at D = 64 on MI355X (8-wave barriers, more idle waves on the
+// causal diagonal), and do not fit LDS at D = 128: 4 everywhere.
+template <int D>
+__host__ __device__ constexpr int bwd_waves() { return 4; }
+
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnParams p) {
-  constexpr int BNK = 128, BMQ = 32, NCH = D / 8;
+__global__ __launch_bounds__(bwd_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnParams p) {
+  constexpr int NW = bwd_waves<D>(), NT = NW * 64;
+  constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8;
   constexpr int KT = BNK * D;  // K image elements
   constexpr int QT = BMQ * D;  // Q / dO tile elements
-  constexpr int NSTQ = BMQ * NCH / 256;  // 16-byte chunks per thread per Q/dO tile
+  constexpr int NQC = BMQ * NCH;          // 16-byte chunks per Q (or dO) tile
+  constexpr int NSTQ = 2 * NQC / NT;      // chunks per thread per Q+dO stage
+  static_assert(NSTQ * NT == 2 * NQC, "Q/dO staging must divide over the threads");
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Ks = smem;                       // [128][D]
+  bf16_t* Ks = smem;                       // [BNK][D]
   bf16_t* Qs = Ks + KT;                    // [2][32][D]
   bf16_t* Ds = Qs + 2 * QT;                // [2][32][D]  (dO)
-  bf16_t* St = Ds + 2 * QT;                // [4 waves][32 keys][32 q]
-  float* lse_s = reinterpret_cast<float*>(St + 4 * 32 * 32);  // [2][32]
-  float* del_s = lse_s + 64;                                  // [2][32]
+  bf16_t* St = Ds + 2 * QT;                // [NW waves][32 keys][32 q]
+  float* lse_s = reinterpret_cast<float*>(St + NW * 32 * 32);  // [2][32]
+  float* del_s = lse_s + 64;                                   // [2][32]
   constexpr int DQP = BMQ + 4;  // padded q-row of the [d][q] dQ partials (conflict-free b128)
-  float* dqr = del_s + 64;                                    // [4][D][DQP]
+  float* dqr = del_s + 64;                                     // [NW][D][DQP]
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h32 = lane >> 5, l32 = lane & 31;
@@ -262,7 +271,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
     }
   }
   // K image for the dQ product (transposed reads)
-  for (int cidx = tid; cidx < BNK * NCH; cidx += 256) {
+  for (int cidx = tid; cidx < BNK * NCH; cidx += NT) {
     const int row = cidx / NCH, ch = cidx % NCH;
     const long key = min(kt0 + row, p.Tk - 1);
     *reinterpret_cast<bf16x8*>(Ks + loff<D>(row, ch * 8)) =
@@ -280,19 +289,27 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
   const int iters_per_head = nqi - qi0;
   const int total = iters_per_head * rep;
 
-  bf16x8 qst[NSTQ], dst[NSTQ];
+  // Q+dO staging registers (NSTQ 16-byte chunks per thread)
+  bf16x8 qdst[NSTQ];
   float lse_r = 0.f, del_r = 0.f;
   auto gload = [&](int it) {
     const int hq = hk * rep + it / iters_per_head;
     const int qbase = (qi0 + it % iters_per_head) * BMQ;
     const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
     const bf16_t* Db = p.dout + b * p.do_sb + hq * p.do_sh;
+    if constexpr (NSTQ >= 2) {  // each thread: NSTQ/2 chunks of Q and the same of dO
 #pragma unroll
-    for (int i = 0; i < NSTQ; ++i) {
-      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
-      const long q = min(qbase + row, p.T - 1);
-      qst[i] = *reinterpret_cast<const bf16x8*>(Qb + q * p.q_st + ch * 8);
-      dst[i] = *reinterpret_cast<const bf16x8*>(Db + q * p.do_st + ch * 8);
+      for (int i = 0; i < NSTQ / 2; ++i) {
+        const int c = tid + i * NT, row = c / NCH, ch = c % NCH;
+        const long q = min(qbase + row, p.T - 1);
+        qdst[i] = *reinterpret_cast<const bf16x8*>(Qb + q * p.q_st + ch * 8);
+        qdst[NSTQ / 2 + i] = *reinterpret_cast<const bf16x8*>(Db + q * p.do_st + ch * 8);
+      }
+    } else {  // one chunk per thread: the first NQC threads take Q, the rest dO
+      const int isd = tid >= NQC, w = tid - isd * NQC;
+      const long q = min(qbase + w / NCH, p.T - 1);
+      const bf16_t* src = isd ? Db + q * p.do_st : Qb + q * p.q_st;
+      qdst[0] = *reinterpret_cast<const bf16x8*>(src + (w % NCH) * 8);
     }
     if (tid < 32) {
       const long q = min(qbase + tid, p.T - 1);
@@ -302,12 +319,16 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
     }
   };
   auto swrite = [&](int buf) {
+    if constexpr (NSTQ >= 2) {
 #pragma unroll
-    for (int i = 0; i < NSTQ; ++i) {
-      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
-      const int o = loff<D>(row, ch * 8);
-      *reinterpret_cast<bf16x8*>(Qs + buf * QT + o) = qst[i];
-      *reinterpret_cast<bf16x8*>(Ds + buf * QT + o) = dst[i];
+      for (int i = 0; i < NSTQ / 2; ++i) {
+        const int c = tid + i * NT, o = loff<D>(c / NCH, (c % NCH) * 8);
+        *reinterpret_cast<bf16x8*>(Qs + buf * QT + o) = qdst[i];
+        *reinterpret_cast<bf16x8*>(Ds + buf * QT + o) = qdst[NSTQ / 2 + i];
+      }
+    } else {
+      const int isd = tid >= NQC, w = tid - isd * NQC;
+      *reinterpret_cast<bf16x8*>((isd ? Ds : Qs) + buf * QT + loff<D>(w / NCH, (w % NCH) * 8)) = qdst[0];
     }
     if (tid < 32) {
       lse_s[buf * 32 + tid] = lse_r;
@@ -372,14 +393,16 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
           dva[db] = mfma32(tr_frag<D>(Dc, 16 * s2 + 4 * h32, db * 32, lane, 8), pb[s2], dva[db]);
           dka[db] = mfma32(tr_frag<D>(Qc, 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
         }
-      // dS^T image [key][q] (64-byte rows, unswizzled: the transposed read of 4 rows x 32
-      // columns covers all 64 banks exactly once); the bf16 values are the sb fragments
+      // dS^T image [key][q]: 64-byte rows of eight 8-byte chunks (4 q each), chunk c of
+      // row k stored at c ^ ((k>>1)&7).  The ds_write_b64 of 16 consecutive keys was 8-way
+      // bank-conflicted unswizzled (PMC: 31% of LDS cycles were conflicts); the transposed
+      // read (4 whole rows per half-wave) is conflict-free either way.
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         bf16x4 v4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v4[j] = sb[g4 >> 1][4 * (g4 & 1) + j];
-        *reinterpret_cast<bf16x4*>(Sw + l32 * 32 + 8 * g4 + 4 * h32) = v4;
+        *reinterpret_cast<bf16x4*>(Sw + l32 * 32 + 4 * ((2 * g4 + h32) ^ ((l32 >> 1) & 7))) = v4;
       }
       // dQ partial = dS K over this wave's 32 keys (A and B both by transposed reads)
       {
@@ -390,7 +413,8 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
         for (int s3 = 0; s3 < 2; ++s3) {
           const int krow = 16 * s3 + 8 * h32 + (i >> 2);
           const int qcol = 16 * (g & 1) + 4 * (i & 3);
-          const bf16x8 a = cat8(lds_tr(Sw, krow * 32 + qcol), lds_tr(Sw, (krow + 4) * 32 + qcol));
+          const bf16x8 a = cat8(lds_tr(Sw, krow * 32 + 4 * ((qcol >> 2) ^ ((krow >> 1) & 7))),
+                                lds_tr(Sw, (krow + 4) * 32 + 4 * ((qcol >> 2) ^ (((krow + 4) >> 1) & 7))));
 #pragma unroll
           for (int db = 0; db < D / 32; ++db) {
             const bf16x8 bk = tr_frag<D>(Ks, wv * 32 + 16 * s3 + 8 * h32, db * 32, lane, 4);
@@ -415,18 +439,19 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_kernel(AttnPa
       }
     if (it + 1 < total) swrite(buf ^ 1);
     __syncthreads();
-    // fold the 4 waves (16-byte reads of 4 q's) and add scale * sum to the fp32 dQ
+    // fold the NW waves (16-byte reads of 4 q's) and add scale * sum to the fp32 dQ
     // accumulator: lanes run over d, so each atomic instruction covers D contiguous floats
     {
       float* dqg = p.dq_acc + (((long)b * p.Hq + hq) * p.T) * D;
+      static_assert((BMQ * D / 4) % NT == 0, "fold groups must divide over the threads");
 #pragma unroll
-      for (int k = 0; k < D / 32; ++k) {
-        const int e = tid + k * 256;
+      for (int k = 0; k < BMQ * D / 4 / NT; ++k) {
+        const int e = tid + k * NT;
         const int d = e % D, qg = e / D;
         const int o = d * DQP + 4 * qg;
         f32x4 sum = *reinterpret_cast<const f32x4*>(dqr + o);
 #pragma unroll
-        for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const f32x4*>(dqr + w * D * DQP + o);
+        for (int w = 1; w < NW; ++w) sum += *reinterpret_cast<const f32x4*>(dqr + w * D * DQP + o);
         if (!(p.flags & 1)) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -488,7 +513,8 @@ extern "C++" {
 
 static size_t fwd_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
 static size_t bwd_lds(int D) {
-  return (size_t)128 * D * 2 + 4 * 32 * D * 2 + 4 * 32 * 32 * 2 + 128 * 4 + 4 * D * (32 + 4) * 4;
+  const size_t nw = D == 64 ? bwd_waves<64>() : bwd_waves<128>();
+  return 32 * nw * D * 2 + 4 * 32 * D * 2 + nw * 32 * 32 * 2 + 128 * 4 + nw * D * (32 + 4) * 4;
 }
 
 template <int D, bool CAUSAL>
@@ -530,10 +556,11 @@ int orion_attn_bwd(const AttnParams& p, int D, bool causal, float* delta, hipStr
   else return -1;
   AttnParams q = p;
   q.delta = delta;
-  const int grid = ((p.Tk + 127) / 128) * p.B * p.Hkv;
 #define BWD(DD, CC)                                                                 \
   set_lds_attr<DD, CC>();                                                           \
-  attn_bwd_kernel<DD, CC><<<grid, 256, bwd_lds(DD), st>>>(q);
+  attn_bwd_kernel<DD, CC><<<((p.Tk + 32 * bwd_waves<DD>() - 1) / (32 * bwd_waves<DD>())) * \
+                                p.B * p.Hkv,                                        \
+                            64 * bwd_waves<DD>(), bwd_lds(DD), st>>>(q);
   if (D == 64) {
     if (causal) { BWD(64, true) } else { BWD(64, false) }
   } else {
