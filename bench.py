@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-tuned-gemms", action="store_true",
                     help="do not load the committed TunableOp GEMM table (orion_amd/tuning/)")
     ap.add_argument("--gemm-table", default=None, help="TunableOp table to load instead of the committed one")
+    ap.add_argument("--hip-graph", action="store_true",
+                    help="capture the whole training step in a HIP graph (single GPU)")
     return ap.parse_args()
 
 
@@ -92,7 +94,7 @@ def main():
 
     ocfg = OptimConfig(warmup_iters=10, lr_decay_iters=10000)
     if args.impl == "native":
-        trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb)
+        trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb, graph=args.hip_graph and world == 1)
         step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
     else:
         ddp_model = model
@@ -164,6 +166,7 @@ def main():
             "data": "synthetic (random token ids), random-init weights",
             "impl": args.impl,
             "tuned_gemm_entries": n_tuned,
+            "hip_graph": bool(args.hip_graph and world == 1 and args.impl == "native"),
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
             "loss": round(final_loss, 4),
             "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),

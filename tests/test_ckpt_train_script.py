@@ -69,3 +69,14 @@ def test_llama_checkpoint_roundtrip(tmp_path):
     m2 = build_model_from_checkpoint(load_checkpoint(p))
     for (n, a), (_, b) in zip(m.named_parameters(), m2.named_parameters()):
         assert torch.allclose(a.float(), b.float()), n
+
+
+def test_train_profiler_trace(tmp_path):
+    """profile_steps > 0 writes a Chrome trace of that many steps (SURVEY.md §5 tracing)."""
+    _run([os.path.join(ROOT, "train.py"), "--device=cpu", "--model=gpt2-tiny", "--n_layer=1", "--n_head=2",
+          "--n_embd=64", "--block_size=16", "--batch_size=2", "--gradient_accumulation_steps=1",
+          "--max_iters=4", "--eval_interval=4", "--eval_iters=1", f"--out_dir={tmp_path}/o", "--dataset=",
+          "--profile_start=1", "--profile_steps=2"], str(tmp_path))
+    import json
+    trace = json.loads((tmp_path / "o" / "trace_rank0.json").read_text())
+    assert trace["traceEvents"]

@@ -386,3 +386,23 @@ def test_xent_ignore_index_and_unaligned_targets():
     lr_.backward()
     assert abs(loss.item() - lr_.item()) < 2e-2
     assert rel_err(x.grad, xr.grad) < 2e-2 and rel_err(w.grad, wr.grad) < 2e-2
+
+
+def test_trainer_hip_graph_matches_eager():
+    """the graph-captured step (warm-up, capture, replays) follows the eager trajectory."""
+    from orion_amd.models.gpt2 import build_gpt2
+    from orion_amd.train.engine import Trainer, OptimConfig
+    cfg = OptimConfig(warmup_iters=2, lr_decay_iters=20, learning_rate=1e-3)
+    torch.manual_seed(0)
+    batches = [[(torch.randint(0, 512, (4, 64), device=DEV), torch.randint(0, 512, (4, 64), device=DEV))
+                for _ in range(2)] for _ in range(6)]
+    losses = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        m = build_gpt2("gpt2-tiny", vocab_size=512, block_size=64).to(DEV)
+        tr = Trainer(m, cfg, graph=graph)
+        losses[graph] = [float(tr.step(b)) for b in batches]
+        if graph:
+            assert tr._graph is not None
+    for a, b in zip(losses[False], losses[True]):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (losses[False], losses[True])

@@ -42,6 +42,9 @@ DEFAULTS = dict(
     grad_clip=1.0, decay_lr=True, warmup_iters=2000, lr_decay_iters=600000, min_lr=6e-5,
     backend="nccl", device="cuda", dtype="bfloat16", seed=1337, bucket_mb=64.0,
     data_root="data",
+    # tracing: profile_steps > 0 records that many steps, starting at
+    # profile_start, with torch.profiler and writes a Chrome trace to out_dir
+    profile_start=10, profile_steps=0, peak_flops=2.5e15,
 )
 
 
@@ -167,6 +170,19 @@ def main(argv=None):
         model.train()
         return out
 
+    flops_per_tok = model.flops_per_token(T) if hasattr(model, "flops_per_token") else 0.0
+    prof = None
+    if cfg["profile_steps"] > 0 and master:
+        acts = [torch.profiler.ProfilerActivity.CPU]
+        if device.type == "cuda":
+            acts.append(torch.profiler.ProfilerActivity.CUDA)
+        prof = torch.profiler.profile(
+            activities=acts,
+            schedule=torch.profiler.schedule(wait=max(0, cfg["profile_start"] - 1), warmup=1,
+                                             active=cfg["profile_steps"], repeat=1),
+            on_trace_ready=lambda p: p.export_chrome_trace(
+                os.path.join(cfg["out_dir"], f"trace_rank{rank}.json")))
+        prof.start()
     t0 = time.time()
     last_losses = {}
     while True:
@@ -183,14 +199,21 @@ def main(argv=None):
                 break
         batches = [train_src.next() for _ in range(A)]
         loss = trainer.step(batches)
+        if prof is not None:
+            prof.step()
         if it % cfg["log_interval"] == 0 and master:
             lossf = float(loss)
             dt = time.time() - t0
             t0 = time.time()
             tps = tokens_per_iter / dt if it > 0 else 0.0
+            mfu = tps / world * flops_per_tok / cfg["peak_flops"]
+            mem = (f", mem {torch.cuda.max_memory_allocated(device) / 2**30:.1f} GiB"
+                   if device.type == "cuda" else "")
             print(f"iter {it}: loss {lossf:.4f}, time {dt * 1000:.2f}ms, lr {trainer.opt.lr:.2e}, "
-                  f"tok/s {tps:,.0f}", flush=True)
+                  f"tok/s {tps:,.0f}, mfu {100 * mfu:.1f}%{mem}", flush=True)
 
+    if prof is not None:
+        prof.stop()
     if master and os.environ.get("METAOPT_RESULTS_PATH"):
         from orion_amd.client import report_results
         report_results([dict(name="val_loss", type="objective", value=float(last_losses.get("val", best_val)))])
