@@ -65,7 +65,9 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     n_tuned = 0
-    if not args.no_tuned_gemms:
+    # TunableOp's table is not applied under HIP-graph capture (solutions chosen by index
+    # went wrong on replay in testing); graph runs use hipBLASLt's default heuristics
+    if not args.no_tuned_gemms and not args.hip_graph:
         from orion_amd.tuning import use_tuned_gemms
         n_tuned = use_tuned_gemms(args.gemm_table, verbose=(rank == 0))
     torch.manual_seed(1337 + rank)

@@ -46,7 +46,7 @@ class GPTConfig:
 
 PRESETS = {
     # BASELINE.json config 1: CPU plumbing model
-    "gpt2-tiny": dict(n_layer=2, n_head=4, n_embd=128, block_size=256),
+    "gpt2-tiny": dict(n_layer=2, n_head=2, n_embd=128, block_size=256),  # head dim 64 (HIP attention: 64/128)
     "gpt2": dict(n_layer=12, n_head=12, n_embd=768),            # 124M
     "gpt2-medium": dict(n_layer=24, n_head=16, n_embd=1024),    # 350M
     "gpt2-large": dict(n_layer=36, n_head=20, n_embd=1280),     # 774M

@@ -388,18 +388,21 @@ def test_xent_ignore_index_and_unaligned_targets():
     assert rel_err(x.grad, xr.grad) < 2e-2 and rel_err(w.grad, wr.grad) < 2e-2
 
 
-def test_trainer_hip_graph_matches_eager():
-    """the graph-captured step (warm-up, capture, replays) follows the eager trajectory."""
+@pytest.mark.parametrize("shape", [("gpt2-tiny", 4, 64, 2, {}), ("gpt2", 8, 1024, 1, dict(n_layer=2))])
+def test_trainer_hip_graph_matches_eager(shape):
+    """the graph-captured step (warm-up, capture, replays) follows the eager trajectory;
+    the GPT-2-width case exercises the split-K wgrad slabs and the attention atomics."""
     from orion_amd.models.gpt2 import build_gpt2
     from orion_amd.train.engine import Trainer, OptimConfig
+    name, B, T, A, over = shape
     cfg = OptimConfig(warmup_iters=2, lr_decay_iters=20, learning_rate=1e-3)
     torch.manual_seed(0)
-    batches = [[(torch.randint(0, 512, (4, 64), device=DEV), torch.randint(0, 512, (4, 64), device=DEV))
-                for _ in range(2)] for _ in range(6)]
+    batches = [[(torch.randint(0, 512, (B, T), device=DEV), torch.randint(0, 512, (B, T), device=DEV))
+                for _ in range(A)] for _ in range(6)]
     losses = {}
     for graph in (False, True):
         torch.manual_seed(0)
-        m = build_gpt2("gpt2-tiny", vocab_size=512, block_size=64).to(DEV)
+        m = build_gpt2(name, vocab_size=512, block_size=T, **over).to(DEV)
         tr = Trainer(m, cfg, graph=graph)
         losses[graph] = [float(tr.step(b)) for b in batches]
         if graph:
