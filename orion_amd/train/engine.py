@@ -9,6 +9,7 @@ is returned as a device tensor.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -53,6 +54,11 @@ class Trainer:
     what bounds small models and small micro-batches."""
 
     GRAPH_WARMUP = 2
+    # BLAS library for captured steps: "cublas" (= rocBLAS on ROCm) or "cublaslt"
+    # (hipBLASLt).  Replaying a capture of the 12-layer GPT-2 step at 65k tokens hit an
+    # illegal address with hipBLASLt's large-shape kernels (small shapes replayed fine),
+    # so captured steps use rocBLAS unless ORION_GRAPH_BLAS says otherwise.
+    GRAPH_BLAS = os.environ.get("ORION_GRAPH_BLAS", "cublas")
 
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float = 64.0, arena_dtype=None,
@@ -120,6 +126,8 @@ class Trainer:
 
     def _step_graph(self, batches):
         self.opt.set_lr(cosine_lr(self.iter_num, self.cfg))
+        if self._graph is None and self.iter_num == 0 and self.GRAPH_BLAS:
+            torch.backends.cuda.preferred_blas_library(self.GRAPH_BLAS)
         if self._graph is None and self.iter_num < self.GRAPH_WARMUP:
             # eager warm-up on a side stream: lazy inits (kernel attributes, TunableOp
             # lookups, allocator pools) must not happen inside the capture
