@@ -125,14 +125,19 @@ def main():
             dist.barrier()
 
     loss = None
+    trace = os.environ.get("ORION_BENCH_TRACE_LOSS") == "1"  # debugging: per-step loss (syncs)
     for i in range(args.warmup):
         loss = step_fn(i)
+        if trace:
+            print(f"warmup {i} loss {float(loss):.4f}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step_fn(args.warmup + i)
+        if trace:
+            print(f"step {i} loss {float(loss):.4f}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -168,7 +173,7 @@ def main():
             "data": "synthetic (random token ids), random-init weights",
             "impl": args.impl,
             "tuned_gemm_entries": n_tuned,
-            "hip_graph": bool(args.hip_graph and world == 1 and args.impl == "native"),
+            "hip_graph": bool(args.impl == "native" and trainer.graph_enabled),
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
             "loss": round(final_loss, 4),
             "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),

@@ -197,7 +197,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
 }
 
 // ============================================================================ backward prep
-// delta[b][h][t] = sum_d dO * O ; 8 bf16 per lane, D/8 lanes per row.
+// delta[b][h][t] = sum_d dO * O ; 8 bf16 per lane, D/8 lanes per row.  Also zeroes the
+// row's fp32 dQ accumulator (the backward adds into it with atomics): a kernel, not a
+// hipMemsetAsync -- inside a captured HIP graph the memset node raced the atomics
+// (wrong / NaN gradients on replay that came and went with timing).
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnParams p, float* delta) {
   constexpr int TPR = D / 8;  // threads per row
@@ -217,7 +220,12 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnParams p, float* 
   }
 #pragma unroll
   for (int o2 = TPR / 2; o2 > 0; o2 >>= 1) s += __shfl_xor(s, o2, 64);
-  if (row < nrows && sub == 0) delta[row] = s;
+  if (row < nrows) {
+    if (sub == 0) delta[row] = s;
+    f32x4* z = reinterpret_cast<f32x4*>(p.dq_acc + row * D + sub * 8);
+    z[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    z[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 }
 
 // ============================================================================ backward
@@ -549,7 +557,6 @@ int orion_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {
 int orion_attn_bwd(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
   const long rows = (long)p.B * p.Hq * p.T;
   const long threads = rows * (D / 8);
-  hipMemsetAsync(p.dq_acc, 0, (size_t)rows * D * sizeof(float), st);
   const int pre_grid = (int)((threads + 255) / 256);
   if (D == 64) attn_bwd_pre_kernel<64><<<pre_grid, 256, 0, st>>>(p, delta);
   else if (D == 128) attn_bwd_pre_kernel<128><<<pre_grid, 256, 0, st>>>(p, delta);

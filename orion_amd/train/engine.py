@@ -32,6 +32,9 @@ class OptimConfig:
     decay_lr: bool = True
 
 
+_GRAPH_SYNC = os.environ.get("ORION_GRAPH_SYNC") == "1"  # debugging aid
+
+
 def cosine_lr(it: int, cfg: OptimConfig) -> float:
     """nanoGPT's schedule: linear warmup, cosine decay to min_lr."""
     if not cfg.decay_lr:
@@ -54,11 +57,13 @@ class Trainer:
     what bounds small models and small micro-batches."""
 
     GRAPH_WARMUP = 2
-    # BLAS library for captured steps: "cublas" (= rocBLAS on ROCm) or "cublaslt"
-    # (hipBLASLt).  Replaying a capture of the 12-layer GPT-2 step at 65k tokens hit an
-    # illegal address with hipBLASLt's large-shape kernels (small shapes replayed fine),
-    # so captured steps use rocBLAS unless ORION_GRAPH_BLAS says otherwise.
-    GRAPH_BLAS = os.environ.get("ORION_GRAPH_BLAS", "cublas")
+    # Captured steps are validated against eager (same loss trajectory) up to 8192 tokens
+    # per micro-batch.  At 65,536 tokens the third replay of the 12-layer GPT-2 step hits
+    # a memory-aperture violation inside the library GEMMs (our kernels have no host-side
+    # state in the graph since the dQ zeroing moved out of hipMemsetAsync), and routing the
+    # capture through rocBLAS gave NaNs even at small shapes -- so larger micro-batches run
+    # eagerly, where launch overhead is < 0.2 % of the step anyway.
+    GRAPH_MAX_TOKENS = int(os.environ.get("ORION_GRAPH_MAX_TOKENS", 8192))
 
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float = 64.0, arena_dtype=None,
@@ -91,6 +96,10 @@ class Trainer:
 
     def step(self, batches):
         """batches: sequence of (idx, targets) micro-batches.  Returns mean loss (device)."""
+        if self.graph_enabled and self._graph is None and batches[0][0].numel() > self.GRAPH_MAX_TOKENS:
+            print(f"[orion_amd] HIP-graph capture is validated up to {self.GRAPH_MAX_TOKENS} tokens "
+                  f"per micro-batch; running {batches[0][0].numel()} eagerly", flush=True)
+            self.graph_enabled = False
         if self.graph_enabled:
             return self._step_graph(batches)
         return self._step_eager(batches)
@@ -126,8 +135,6 @@ class Trainer:
 
     def _step_graph(self, batches):
         self.opt.set_lr(cosine_lr(self.iter_num, self.cfg))
-        if self._graph is None and self.iter_num == 0 and self.GRAPH_BLAS:
-            torch.backends.cuda.preferred_blas_library(self.GRAPH_BLAS)
         if self._graph is None and self.iter_num < self.GRAPH_WARMUP:
             # eager warm-up on a side stream: lazy inits (kernel attributes, TunableOp
             # lookups, allocator pools) must not happen inside the capture
@@ -156,6 +163,8 @@ class Trainer:
                 sy.copy_(y, non_blocking=True)
             self.opt.hyper_tensor()
         self._graph.replay()
+        if _GRAPH_SYNC:
+            torch.cuda.synchronize()
         self.opt.step_count += 1
         self.iter_num += 1
         return self._static_loss
