@@ -211,15 +211,19 @@ __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
 }
 
 // kernel configurations: {KS, NS}; LDS = NS * KS * 32 KB <= 160 KB
+// (A cross-stage fragment-prefetch variant -- barrier for stage t+1 before the MFMAs of
+// stage t, second fragment register set -- measured 0.77-0.79 PF/s vs 0.95-0.99 for
+// config 0 on MI355X and was removed; docs/PERFORMANCE.md.)
 struct WgCfg { int ks, ns, wm; };
 constexpr WgCfg WG_CFGS[] = {{2, 4, 4}, {2, 4, 2}, {4, 2, 2}, {2, 2, 4}};
+constexpr int WG_NCFG = sizeof(WG_CFGS) / sizeof(WG_CFGS[0]);
 
 static int wg_cfg() {
   static int c = -1;
   if (c < 0) {
     const char* e = getenv("ORION_WGRAD_CFG");
     c = e ? atoi(e) : 0;
-    if (c < 0 || c > 3) c = 0;
+    if (c < 0 || c >= WG_NCFG) c = 0;
   }
   return c;
 }
@@ -285,23 +289,23 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   auto Bb = (const bf16_t*)B;
   float* sl = S > 1 ? slabs : nullptr;
   auto O = (bf16_t*)out;
-#define WG_LAUNCH(KS, NS, WM)                                                                   \
+#define WG_LAUNCH(KERNEL, KS, NS, WM)                                                           \
   {                                                                                             \
     static bool attr = false;                                                                   \
     if (!attr) {                                                                                \
-      if (hipFuncSetAttribute((const void*)wgrad_kernel<KS, NS, WM>,                            \
+      if (hipFuncSetAttribute((const void*)KERNEL<KS, NS, WM>,                                  \
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)   \
         return -5;                                                                              \
       attr = true;                                                                              \
     }                                                                                           \
-    wgrad_kernel<KS, NS, WM><<<ntiles * S, WM * 256, lds, st>>>(Ab, lda, Bb, ldb, M, N1, N2, t2, \
-                                                                ntiles, chunk, sl, O, scale);  \
+    KERNEL<KS, NS, WM><<<ntiles * S, WM * 256, lds, st>>>(Ab, lda, Bb, ldb, M, N1, N2, t2,       \
+                                                          ntiles, chunk, sl, O, scale);         \
   }
   switch (wg_cfg()) {
-    case 0: WG_LAUNCH(2, 4, 4) break;  // measured best on MI355X (16 waves, 122 VGPR)
-    case 1: WG_LAUNCH(2, 4, 2) break;
-    case 2: WG_LAUNCH(4, 2, 2) break;
-    default: WG_LAUNCH(2, 2, 4) break;
+    case 0: WG_LAUNCH(wgrad_kernel, 2, 4, 4) break;  // measured best on MI355X (16 waves, 122 VGPR)
+    case 1: WG_LAUNCH(wgrad_kernel, 2, 4, 2) break;
+    case 2: WG_LAUNCH(wgrad_kernel, 4, 2, 2) break;
+    default: WG_LAUNCH(wgrad_kernel, 2, 2, 4) break;
   }
 #undef WG_LAUNCH
   return (int)hipGetLastError();
