@@ -196,6 +196,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
   }
 }
 
+// Workgroup barrier that orders LDS traffic only.  __syncthreads() also emits
+// s_waitcnt vmcnt(0), which in the backward made every query-tile iteration wait for
+// its own dQ atomics to complete (a full atomic round trip per iteration); the atomics
+// have no reader inside the kernel, so they may stay in flight across the barrier.
+// The "memory" clobber keeps the compiler from moving LDS accesses across it.
+ORION_DEVICE void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ============================================================================ backward prep
 // delta[b][h][t] = sum_d dO * O ; 8 bf16 per lane, D/8 lanes per row.  Also zeroes the
 // row's fp32 dQ accumulator (the backward adds into it with atomics): a kernel, not a
@@ -446,7 +453,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_b
         *reinterpret_cast<f32x4*>(dqw + (db * 32 + l32) * DQP + 8 * g4 + 4 * h32) = v;
       }
     if (it + 1 < total) swrite(buf ^ 1);
-    __syncthreads();
+    lds_barrier();
     // fold the NW waves (16-byte reads of 4 q's) and add scale * sum to the fp32 dQ
     // accumulator: lanes run over d, so each atomic instruction covers D contiguous floats
     {
@@ -469,7 +476,7 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_b
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
