@@ -9,5 +9,5 @@ timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || { tail 
 tail -1 gpurun_out/bench_default.log | cut -c1-200
 rm -rf gpurun_out/prof
 bash scripts/profile.sh --steps 5 --warmup 3 > gpurun_out/profile_run.log 2>&1 || { tail -20 gpurun_out/profile_run.log; exit 1; }
-python scripts/prof_summary.py gpurun_out/prof/run_kernel_stats.csv --steps 5 > gpurun_out/prof_summary.txt
+python scripts/prof_summary.py gpurun_out/prof/run_kernel_stats.csv --steps 8 > gpurun_out/prof_summary.txt
 head -25 gpurun_out/prof_summary.txt; tail -2 gpurun_out/prof_summary.txt

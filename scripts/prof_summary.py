@@ -21,7 +21,7 @@ def short(name):
 
 
 def category(s):
-    if s.startswith("gemm"):
+    if s.startswith("gemm") or s.startswith("wgrad"):
         return "gemm"
     for k in ("attn", "xent", "ln_", "gelu", "colsum", "slab_sum", "adamw", "sumsq", "rms", "rope", "swiglu"):
         if k in s:
