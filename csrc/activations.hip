@@ -129,14 +129,21 @@ __global__ __launch_bounds__(256) void scale_bf16_kernel(bf16_t* __restrict__ x,
 // 1/n_valid * upstream-grad scale folded in.  Fixed summation order: deterministic.
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slabs, int S,
                                                        long n4, bf16_t* __restrict__ out,
-                                                       const float* __restrict__ scale) {
+                                                       const float* __restrict__ scale,
+                                                       int accumulate) {
   const float sc = scale ? *scale : 1.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     f32x4 acc = reinterpret_cast<const f32x4*>(slabs)[i];
     for (int k = 1; k < S; ++k) acc += reinterpret_cast<const f32x4*>(slabs + (long)k * n4 * 4)[i];
     bf16x4 o;
+    if (accumulate) {  // += into the gradient arena (micro-batch accumulation, tied weights)
+      const bf16x4 prev = reinterpret_cast<const bf16x4*>(out)[i];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[j] * sc);
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(fmaf(acc[j], sc, bf2f(prev[j])));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[j] * sc);
+    }
     reinterpret_cast<bf16x4*>(out)[i] = o;
   }
 }
@@ -193,9 +200,10 @@ int orion_scale_bf16(void* x, const float* scale, long n, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-int orion_slab_sum(const float* slabs, int S, long n, void* out, const float* scale, hipStream_t st) {
+int orion_slab_sum(const float* slabs, int S, long n, void* out, const float* scale,
+                   int accumulate, hipStream_t st) {
   if (n % 4) return -1;
   const long n4 = n / 4;
-  slab_sum_kernel<<<ew_grid(n4 / 2), 256, 0, st>>>(slabs, S, n4, (bf16_t*)out, scale);
+  slab_sum_kernel<<<ew_grid(n4 / 2), 256, 0, st>>>(slabs, S, n4, (bf16_t*)out, scale, accumulate);
   return (int)hipGetLastError();
 }

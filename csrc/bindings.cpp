@@ -29,11 +29,11 @@ int orion_colsum_scratch(int rows, int C);
 int orion_swiglu_fwd(const void*, void*, long, int, hipStream_t);
 int orion_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_scale_bf16(void*, const float*, long, hipStream_t);
-int orion_slab_sum(const float*, int, long, void*, const float*, hipStream_t);
+int orion_slab_sum(const float*, int, long, void*, const float*, int, hipStream_t);
 int orion_wgrad_splits(int, int, int);
 int orion_wgrad_effective_splits(int, int);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
-                const float*, hipStream_t);
+                const float*, int, hipStream_t);
 int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
 int orion_sumsq_partials();
 int orion_grad_sumsq(const void*, long, float*, float*, hipStream_t);
@@ -44,8 +44,8 @@ int orion_rmsnorm_fwd(const void*, const void*, void*, float*, int, int, float, 
 int orion_rmsnorm_bwd_blocks(int rows);
 int orion_rmsnorm_bwd(const void*, const void*, const void*, const float*, void*, void*, float*,
                       int, int, const void*, hipStream_t);
-int orion_rope(const void*, long, long, long, void*, const float*, const float*, int, int, int,
-               int, int, float, hipStream_t);
+int orion_rope(const void*, long, long, long, void*, long, long, long, const float*, const float*,
+               int, int, int, int, int, float, hipStream_t);
 int orion_attn_fwd(const orion::AttnParams&, int, bool, hipStream_t);
 int orion_attn_bwd(const orion::AttnParams&, int, bool, float*, hipStream_t);
 int orion_attn_dq_convert(const float*, void*, long, long, long, int, int, int, int, hipStream_t);
@@ -287,36 +287,46 @@ Tensor slab_sum(const Tensor& slabs, const c10::optional<Tensor>& scale) {
     TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "scale must be one fp32");
     sc = scale->data_ptr<float>();
   }
-  check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc, cur_stream()),
+  check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc, 0,
+                              cur_stream()),
                "slab_sum");
   return out;
 }
 
-// dW = dy^T x over the token dim (csrc/wgrad.hip); splits = 0 picks the split-K count
-Tensor wgrad(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& scale, int64_t splits) {
+// dW = dy^T x over the token dim (csrc/wgrad.hip) into out (N1, N2) contiguous bf16:
+// overwritten, or added to when accumulate (the gradient arena across micro-batches / tied
+// weights).  splits = 0 picks the split-K count.
+void wgrad_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& scale, Tensor out,
+                bool accumulate, int64_t splits) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
+  check_bf16(out, "out");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad: dy (M,N1), x (M,N2)");
   TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad: rows must be contiguous");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   const int M = dy.size(0), N1 = dy.size(1), N2 = x.size(1);
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (int64_t)N1 * N2, "wgrad: out must be contiguous (N1, N2)");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   int S = splits > 0 ? orion_wgrad_effective_splits(M, (int)splits) : orion_wgrad_splits(M, N1, N2);
   const float* sc = nullptr;
   if (scale.has_value() && scale->defined()) {
     TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "scale must be one fp32");
     sc = scale->data_ptr<float>();
   }
-  auto out = at::empty({N1, N2}, dy.options());
   if (S > 1) {
     auto slabs = at::empty({S, N1, N2}, dy.options().dtype(at::kFloat));
     check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, S,
-                             slabs.data_ptr<float>(), nullptr, nullptr, cur_stream()), "wgrad");
+                             slabs.data_ptr<float>(), nullptr, nullptr, 0, cur_stream()), "wgrad");
     check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc,
-                                cur_stream()), "wgrad slab_sum");
+                                accumulate ? 1 : 0, cur_stream()), "wgrad slab_sum");
   } else {
     check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, 1,
-                             nullptr, out.data_ptr(), sc, cur_stream()), "wgrad");
+                             nullptr, out.data_ptr(), sc, accumulate ? 1 : 0, cur_stream()), "wgrad");
   }
+}
+
+Tensor wgrad(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& scale, int64_t splits) {
+  auto out = at::empty({dy.size(1), x.size(1)}, dy.options());
+  wgrad_into(dy, x, scale, out, false, splits);
   return out;
 }
 
@@ -419,10 +429,25 @@ Tensor rope(const Tensor& x, const Tensor& cosv, const Tensor& sinv, int64_t pos
   TORCH_CHECK(cosv.size(0) >= T + pos0 && cosv.size(1) == D / 2, "rope table too small");
   auto y = at::empty({B, T, H, D}, x.options());
   check_launch(orion_rope(x.data_ptr(), x.stride(0), x.stride(1), x.stride(2), y.data_ptr(),
-                          cosv.data_ptr<float>(), sinv.data_ptr<float>(), B, T, H, D, (int)pos0,
-                          (float)sign, cur_stream()),
+                          y.stride(0), y.stride(1), y.stride(2), cosv.data_ptr<float>(),
+                          sinv.data_ptr<float>(), B, T, H, D, (int)pos0, (float)sign, cur_stream()),
                "rope");
   return y;
+}
+
+// in-place rotation of a strided (B, T, H, D) view (the q|k slice of a packed gradient)
+void rope_(Tensor x, const Tensor& cosv, const Tensor& sinv, int64_t pos0, double sign) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "rope_: x must be (B, T, H, D) with unit stride on D");
+  TORCH_CHECK(cosv.scalar_type() == at::kFloat && cosv.is_contiguous() && sinv.is_contiguous(),
+              "rope tables must be contiguous fp32");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const int B = x.size(0), T = x.size(1), H = x.size(2), D = x.size(3);
+  TORCH_CHECK(cosv.size(0) >= T + pos0 && cosv.size(1) == D / 2, "rope table too small");
+  check_launch(orion_rope(x.data_ptr(), x.stride(0), x.stride(1), x.stride(2), x.data_ptr(),
+                          x.stride(0), x.stride(1), x.stride(2), cosv.data_ptr<float>(),
+                          sinv.data_ptr<float>(), B, T, H, D, (int)pos0, (float)sign, cur_stream()),
+               "rope_");
 }
 
 // ------------------------------------------------------------------ attention
@@ -518,6 +543,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("slab_sum(Tensor slabs, Tensor? scale=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor? scale=None, int splits=0) -> Tensor");
+  m.def("wgrad_into(Tensor dy, Tensor x, Tensor? scale, Tensor(a!) out, bool accumulate, int splits=0) -> ()");
   m.def("wgrad_splits(int M, int N1, int N2) -> int", &wgrad_splits);  // host-only helper
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
@@ -526,6 +552,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
   m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int pos0, float sign) -> Tensor");
+  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int pos0, float sign) -> ()");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int flags=0) -> ()");
 }
@@ -542,6 +569,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("scale_", &scale_);
   m.impl("slab_sum", &slab_sum);
   m.impl("wgrad", &wgrad);
+  m.impl("wgrad_into", &wgrad_into);
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
   m.impl("grad_sumsq", &grad_sumsq);
   m.impl("adamw_flat", &adamw_flat);
@@ -549,6 +577,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.impl("rope", &rope);
+  m.impl("rope_", &rope_);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
 }

@@ -141,8 +141,10 @@ __global__ __launch_bounds__(256) void rms_bwd_kernel(const bf16_t* __restrict__
 
 // out[b,t,h,:] = rope(x[b,t,h,:]); sign = +1 forward, -1 backward (inverse rotation).
 // One thread per 8 rotation pairs.
-__global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ x, long xsb,
-                                                   long xst, long xsh, bf16_t* __restrict__ y,
+// y may alias x (in-place backward on a strided gradient view): every thread reads its
+// 16 elements before writing them and no two threads touch the same element.
+__global__ __launch_bounds__(256) void rope_kernel(const bf16_t* x, long xsb, long xst, long xsh,
+                                                   bf16_t* y, long ysb, long yst, long ysh,
                                                    const float* __restrict__ cosv,
                                                    const float* __restrict__ sinv, int B, int T,
                                                    int H, int D, int pos0, float sign) {
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ x,
     const long t = (row / H) % T;
     const long b = row / ((long)H * T);
     const bf16_t* xp = x + b * xsb + t * xst + h * xsh;
-    bf16_t* yp = y + ((b * T + t) * H + h) * (long)D;
+    bf16_t* yp = y + b * ysb + t * yst + h * ysh;
     float x1[8], x2[8], o1[8], o2[8];
     ld8f(xp + pg * 8, x1);
     ld8f(xp + D / 2 + pg * 8, x2);
@@ -219,14 +221,14 @@ int orion_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float*
   return (int)hipGetLastError();
 }
 
-int orion_rope(const void* x, long xsb, long xst, long xsh, void* y, const float* cosv,
-               const float* sinv, int B, int T, int H, int D, int pos0, float sign,
-               hipStream_t st) {
+int orion_rope(const void* x, long xsb, long xst, long xsh, void* y, long ysb, long yst,
+               long ysh, const float* cosv, const float* sinv, int B, int T, int H, int D,
+               int pos0, float sign, hipStream_t st) {
   if (D % 16) return -1;
   const long n = (long)B * T * H * (D / 16);
   long g = (n + 255) / 256;
   if (g > 4096) g = 4096;
-  rope_kernel<<<(int)g, 256, 0, st>>>((const bf16_t*)x, xsb, xst, xsh, (bf16_t*)y, cosv, sinv, B,
-                                      T, H, D, pos0, sign);
+  rope_kernel<<<(int)g, 256, 0, st>>>((const bf16_t*)x, xsb, xst, xsh, (bf16_t*)y, ysb, yst, ysh,
+                                      cosv, sinv, B, T, H, D, pos0, sign);
   return (int)hipGetLastError();
 }

@@ -83,7 +83,7 @@ template <int KS, int NS, int WM>
 __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
     const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B, long ldb, int M, int N1,
     int N2, int tiles_n2, int ntiles, int chunk, float* __restrict__ slabs,
-    bf16_t* __restrict__ out, const float* __restrict__ scale) {
+    bf16_t* __restrict__ out, const float* __restrict__ scale, int accumulate) {
   constexpr int BK = 16 * KS;        // m rows per stage
   constexpr int IMG = BK * 128;      // one [BK][128] image
   constexpr int STAGE = 4 * IMG;     // A halves 0,1 | B halves 0,1
@@ -204,7 +204,12 @@ __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
         const int n1 = n10 + wr * TA * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
         if (n1 < N1 && n2 < N2) {
           if (sl) sl[(long)n1 * N2 + n2] = acc[a][b][r];
-          else out[(long)n1 * N2 + n2] = f2bf(acc[a][b][r] * sc);
+          else {
+            const long o = (long)n1 * N2 + n2;
+            float v = acc[a][b][r] * sc;
+            if (accumulate) v += bf2f(out[o]);  // gradient accumulation into the arena
+            out[o] = f2bf(v);
+          }
         }
       }
     }
@@ -272,9 +277,10 @@ int orion_wgrad_lds() {
 }
 
 // A (M x N1, ld lda), B (M x N2, ld ldb) bf16 -> slabs (S, N1, N2) fp32 when S > 1
-// (caller folds them), else out (N1, N2) bf16 scaled by *scale (nullable).
+// (caller folds them), else out (N1, N2) bf16 scaled by *scale (nullable), added to the
+// bf16 values already in out when accumulate != 0.
 int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1, int N2, int S,
-                float* slabs, void* out, const float* scale, hipStream_t st) {
+                float* slabs, void* out, const float* scale, int accumulate, hipStream_t st) {
   const int BK = wg_bk();
   if (M % BK || N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || N1 < 8 || N2 < 8) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -2;
@@ -299,7 +305,8 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
       attr = true;                                                                              \
     }                                                                                           \
     KERNEL<KS, NS, WM><<<ntiles * S, WM * 256, lds, st>>>(Ab, lda, Bb, ldb, M, N1, N2, t2,       \
-                                                          ntiles, chunk, sl, O, scale);         \
+                                                          ntiles, chunk, sl, O, scale,          \
+                                                          accumulate);                          \
   }
   switch (wg_cfg()) {
     case 0: WG_LAUNCH(wgrad_kernel, 2, 4, 4) break;  // measured best on MI355X (16 waves, 122 VGPR)

@@ -1,2 +1,5 @@
-"""``orion.core`` entry points -> :mod:`orion_amd.core`."""
+"""``orion.core`` (reference `src/orion/core/__init__.py:16-34`): version and app dirs."""
 from orion_amd import __version__  # noqa: F401
+from orion_amd.core.config import DIRS  # noqa: F401
+
+__descr__ = "Distributed Asynchronous [black-box] Optimization"

@@ -78,10 +78,7 @@ class Attention(nn.Module):
     def forward(self, x, cos, sin, pos0=0):
         B, T, _ = x.shape
         qkv = ops.linear(x, self.qkv_proj.weight).view(B, T, self.n_heads + 2 * self.n_kv, self.hd)
-        q = ops.rope(qkv[:, :, :self.n_heads], cos, sin, pos0)
-        k = ops.rope(qkv[:, :, self.n_heads:self.n_heads + self.n_kv], cos, sin, pos0)
-        v = qkv[:, :, self.n_heads + self.n_kv:]
-        o = ops.attention(q, k, v, causal=True)              # (B, T, Hq, D)
+        o = ops.rope_attention_packed(qkv, self.n_heads, self.n_kv, cos, sin, pos0)  # (B, T, Hq, D)
         return ops.linear(o.reshape(B, T, -1), self.o_proj.weight)
 
 

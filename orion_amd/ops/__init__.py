@@ -147,6 +147,18 @@ def rope(x, cos, sin, pos0=0):
     return ref.rope(x, cos[pos0:], sin[pos0:])
 
 
+def rope_attention_packed(qkv, n_q, n_kv, cos, sin, pos0=0):
+    """Causal attention of (rope(q), rope(k), v) on a packed (B, T, Hq + 2 Hkv, D) projection
+    -> (B, T, Hq, D).  The GPU path is one fused autograd node (no per-view glue)."""
+    b = _gpu(qkv)
+    if b == "hip":
+        from .flash_attn import rope_flash_attention_packed
+        return rope_flash_attention_packed(qkv, n_q, n_kv, cos, sin, pos0)
+    q = rope(qkv[:, :, :n_q], cos, sin, pos0)
+    k = rope(qkv[:, :, n_q:n_q + n_kv], cos, sin, pos0)
+    return attention(q, k, qkv[:, :, n_q + n_kv:], causal=True)
+
+
 # --------------------------------------------------------------------------- attention
 def attention_qkv(qkv, n_head, causal=True):
     """Causal self-attention on a packed (B, T, 3C) projection -> (B, T, C)."""
@@ -206,5 +218,5 @@ def linear_cross_entropy(x, weight, targets, ignore_index=-1):
 __all__ = [
     "set_backend", "backend", "ext_available", "load_ext",
     "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "rope",
-    "attention_qkv", "attention", "cross_entropy", "linear_cross_entropy",
+    "attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "linear_cross_entropy",
 ]

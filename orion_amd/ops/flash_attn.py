@@ -69,3 +69,41 @@ class _Flash(torch.autograd.Function):
 def flash_attention(q, k, v, causal=True):
     """q (B, T, Hq, D), k/v (B, Tk, Hkv, D) with unit stride on D -> (B, T, Hq, D)."""
     return _Flash.apply(q, k, v, causal)
+
+
+class _RopeFlashPacked(torch.autograd.Function):
+    """RoPE + causal flash attention on a packed (B, T, Hq + 2 Hkv, D) QKV projection.
+
+    Forward: ONE rope launch rotates the adjacent q|k head range into a contiguous
+    (B, T, Hq + Hkv, D) buffer; the attention kernel reads q and k as strided views of it
+    and v straight from the projection.  Backward: the attention kernel writes dq, dk and
+    dv into the three head ranges of ONE packed gradient buffer, and one in-place rope
+    launch (inverse rotation) fixes up the dq|dk range -- no zero-fill, slice copies or
+    gradient adds around the kernels (the per-view autograd path cost ~0.8 ms per
+    Llama-7B layer at 16k tokens, more than the rope kernels themselves)."""
+
+    @staticmethod
+    def forward(ctx, qkv, n_q, n_kv, cos, sin, pos0):
+        B, T, H3, D = qkv.shape
+        qk = C().rope(qkv[:, :, :n_q + n_kv], cos, sin, int(pos0), 1.0)
+        scale = 1.0 / math.sqrt(D)
+        v = qkv[:, :, n_q + n_kv:]
+        o, lse = C().attn_fwd(qk[:, :, :n_q], qk[:, :, n_q:], v, True, scale)
+        ctx.save_for_backward(qkv, qk, o, lse, cos, sin)
+        ctx.meta = (n_q, n_kv, int(pos0), scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, qk, o, lse, cos, sin = ctx.saved_tensors
+        n_q, n_kv, pos0, scale = ctx.meta
+        dqkv = torch.empty_like(qkv)
+        C().attn_bwd(do.contiguous(), qk[:, :, :n_q], qk[:, :, n_q:], qkv[:, :, n_q + n_kv:], o, lse,
+                     True, scale, dqkv[:, :, :n_q], dqkv[:, :, n_q:n_q + n_kv], dqkv[:, :, n_q + n_kv:])
+        C().rope_(dqkv[:, :, :n_q + n_kv], cos, sin, pos0, -1.0)
+        return dqkv, None, None, None, None, None
+
+
+def rope_flash_attention_packed(qkv, n_q, n_kv, cos, sin, pos0=0):
+    """qkv (B, T, Hq + 2 Hkv, D) -> causal attention of rope(q), rope(k), v: (B, T, Hq, D)."""
+    return _RopeFlashPacked.apply(qkv, n_q, n_kv, cos, sin, pos0)

@@ -51,8 +51,38 @@ def wgrad_splits(M: int, n1: int, n2: int) -> int:
     return s
 
 
+def _blas_wins(n1: int, n2: int) -> bool:
+    """hipBLASLt beats csrc/wgrad.hip by 5-12 % when both output dims are large (Llama-7B:
+    12288/4096/22016/32000 x 4096 at 4k-16k tokens); the HIP kernel wins by 1.3-2x on the
+    GPT-2 shapes and at 4096 x 11008 (scripts/bench_wgrad_llama.py, profiles/)."""
+    return n1 >= 4096 and n2 >= 4096 and n1 >= n2
+
+
+def wgrad_into(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool,
+               scale: torch.Tensor | None = None):
+    """out (n1, n2) [+]= dy^T x [* scale]: the weight gradient written straight into its
+    slice of the gradient arena (``ops/grad_sink.py``)."""
+    n1, n2 = dy.shape[1], x.shape[1]
+    if scale is None and _blas_wins(n1, n2):
+        o2 = out.view(n1, n2)
+        if accumulate:
+            torch.addmm(o2, dy.t(), x, out=o2)
+        else:
+            torch.mm(dy.t(), x, out=o2)
+    elif _hip_ok(dy, x):
+        C().wgrad_into(dy, x, scale, out.view(n1, n2), bool(accumulate), int(_FORCE or 0))
+    else:
+        g = wgrad(dy, x, scale)
+        if accumulate:
+            out.view(n1, n2).add_(g)
+        else:
+            out.view(n1, n2).copy_(g)
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Tensor:
     """dy (M, n1), x (M, n2) bf16 -> dy^T x (n1, n2) bf16 [times the device scalar ``scale``]."""
+    if scale is None and dy.is_cuda and _blas_wins(dy.shape[1], x.shape[1]):
+        return dy.t() @ x
     if _hip_ok(dy, x):
         return C().wgrad(dy, x, scale, int(_FORCE or 0))
     M, n1 = dy.shape

@@ -6,7 +6,8 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
-from .gemm import wgrad
+from .gemm import wgrad, wgrad_into
+from .grad_sink import sink_of
 
 
 def _bf16(t):
@@ -78,6 +79,7 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.sink = sink_of(w)  # dW straight into the gradient arena (ops/grad_sink.py)
         return torch.nn.functional.linear(x, w, b)
 
     @staticmethod
@@ -88,7 +90,12 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ w).view(x.shape)
         if ctx.needs_input_grad[1]:
-            dw = wgrad(dy2, x.reshape(-1, x.shape[-1]))
+            sink = ctx.sink
+            if sink is not None:
+                wgrad_into(dy2, x.reshape(-1, x.shape[-1]), sink.view, sink.take())
+                sink.notify()
+            else:
+                dw = wgrad(dy2, x.reshape(-1, x.shape[-1]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = C().colsum(dy2.contiguous())
         return dx, dw, db

@@ -10,7 +10,8 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
-from .gemm import wgrad
+from .gemm import wgrad, wgrad_into
+from .grad_sink import sink_of
 
 
 class _LinearXent(torch.autograd.Function):
@@ -19,6 +20,7 @@ class _LinearXent(torch.autograd.Function):
         logits = torch.nn.functional.linear(x, w)
         loss = C().xent_fwd_bwd(logits, targets.contiguous(), int(ignore_index))
         ctx.save_for_backward(x, w, logits)   # logits now hold dlogits / n_valid
+        ctx.sink = sink_of(w)
         return loss
 
     @staticmethod
@@ -30,7 +32,12 @@ class _LinearXent(torch.autograd.Function):
             dx = dl @ w
             C().scale_(dx, s)
         if ctx.needs_input_grad[1]:
-            dw = wgrad(dl, x, s)
+            sink = ctx.sink
+            if sink is not None:
+                wgrad_into(dl, x, sink.view, sink.take(), s)
+                sink.notify()
+            else:
+                dw = wgrad(dl, x, s)
         return dx, dw, None, None
 
 

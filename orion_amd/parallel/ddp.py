@@ -62,6 +62,9 @@ class GradBucketReducer:
         self._sync = True
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._on_grad)
                        for s in arena.slots]
+        # weights whose gradient the GEMM writes straight into the arena (ops/grad_sink.py)
+        # never run AccumulateGrad: their sinks report through the arena's listener list
+        arena.grad_listeners.append(self._on_grad)
         avg = getattr(dist.ReduceOp, "AVG", None)
         self._use_avg_op = average and avg is not None and dist.get_backend(group) == "nccl"
 
@@ -113,6 +116,8 @@ class GradBucketReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self._on_grad in self.arena.grad_listeners:
+            self.arena.grad_listeners.remove(self._on_grad)
 
 
 def all_reduce_scalar(t: torch.Tensor, op="mean", group=None):

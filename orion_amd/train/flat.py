@@ -23,6 +23,8 @@ from dataclasses import dataclass
 import torch
 import torch.nn as nn
 
+from ..ops import grad_sink
+
 ALIGN = 2048  # elements; also the AdamW weight-decay chunk size
 
 
@@ -47,6 +49,9 @@ class FlatArena:
         device = device or next(model.parameters()).device
         grad_dtype = grad_dtype or dtype
         decay_filter = decay_filter or (lambda name, p: p.dim() >= 2)
+        uses: dict[int, int] = {}
+        for _, p in model.named_parameters(remove_duplicate=False):
+            uses[id(p)] = uses.get(id(p), 0) + 1
         seen = set()
         named = []
         for name, p in model.named_parameters():
@@ -81,6 +86,14 @@ class FlatArena:
                 self.init_fp32[s.offset: s.offset + s.numel].copy_(s.param.data.reshape(-1))
                 s.param.data = view
                 s.param.grad = self.grads[s.offset: s.offset + s.numel].view_as(s.param)
+        # direct-to-arena weight gradients (ops/grad_sink.py); tied parameters excluded
+        self.grad_listeners: list = []
+        self.sinks = []
+        for s in slots:
+            if uses.get(id(s.param), 1) == 1:
+                sk = grad_sink.attach(s.param, s.param.grad, self.grad_listeners)
+                if sk is not None:
+                    self.sinks.append(sk)
 
     def param_view(self, slot: ParamSlot):
         return self.params[slot.offset: slot.offset + slot.numel]
@@ -90,6 +103,14 @@ class FlatArena:
 
     def zero_grad(self):
         self.grads.zero_()
+        for sk in self.sinks:
+            sk.fresh = True
+
+    def detach_sinks(self):
+        """Stop direct gradient writes (params then take the AccumulateGrad path)."""
+        for s in self.slots:
+            grad_sink.detach(s.param)
+        self.sinks = []
 
     def rebind_grads(self):
         """Re-point ``p.grad`` at the arena (after anything replaced it)."""
