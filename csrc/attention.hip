@@ -36,6 +36,8 @@
 // which makes BOTH the row reads (ds_read_b128, 16 distinct rows per lane
 // group) and the transposed reads (4 rows x 32 columns per half-wave)
 // conflict-free on the 64-bank LDS.
+#include <type_traits>
+
 #include "common.h"
 #include "attn_params.h"
 #include "mfma_lds.h"
@@ -510,8 +512,8 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_b
 // K from the K image) and adds them with 8 float-atomic instructions.
 //
 // A q slice holds BMQ = 64 rows (two 32-row q blocks).  Per wave and slice: 2 x {S, dP,
-// dV^T, dK^T} (32 v_mfma_f32_32x32x16_bf16) + 16 16x16x32 MFMAs for dQ.  V fragments of
-// the wave's keys live in registers (B operand of dP), K rows come from the LDS image.
+// dV^T, dK^T} (32 v_mfma_f32_32x32x16_bf16) + 16 16x16x32 MFMAs for dQ.  K and V fragments
+// of the wave's keys live in registers (B operands of S and dP).
 // LDS at D = 64: K image 32 KB + Q, dO slices (double-buffered) 32 KB + dS^T image
 // (double-buffered) 64 KB = 128 KB.  One barrier per slice (buffer reuse: loop comment).
 // A 4-wave x 64-key form (one wave per SIMD) measured 1.07 ms vs 0.89 ms for the
@@ -567,18 +569,20 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
   const int kt0 = kt * BNK, kw0 = kt0 + wv * 32;
   const int mykey = kw0 + l32;
   const int off = p.Tk - p.T;
-  const float c = p.scale_log2;
+  const float c = p.scale_log2, inv_c = 1.f / p.scale_log2;
 
   const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
 
-  // V fragments of this wave's 32 keys (B operands of dP), kept in registers
-  bf16x8 vf[D / 16];
+  // K and V fragments of this wave's 32 keys (B operands of S and dP), kept in registers
+  bf16x8 kf[D / 16], vf[D / 16];
   {
     const long key = min(mykey, p.Tk - 1);
 #pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks)
+    for (int ks = 0; ks < D / 16; ++ks) {
+      if (CAUSAL) kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
       vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ks * 16 + 8 * h32);
+    }
   }
   // K image: row reads (B operand of S) and transposed reads (B operand of dQ)
   for (int cidx = tid; cidx < BNK * NCH; cidx += NT) {
@@ -626,9 +630,9 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
       *reinterpret_cast<bf16x8*>(Qs + buf * QT + o) = qdst[i];
       *reinterpret_cast<bf16x8*>(Ds + buf * QT + o) = qdst[NSTQ / 2 + i];
     }
-    if (tid < BMQ) {
-      lse_s[buf * BMQ + tid] = lse_r;
-      del_s[buf * BMQ + tid] = del_r;
+    if (tid < BMQ) {  // row constants as the initial S / dP accumulators (see the loop)
+      lse_s[buf * BMQ + tid] = -lse_r * inv_c;
+      del_s[buf * BMQ + tid] = -del_r;
     }
   };
 
@@ -644,8 +648,10 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
   // before the barrier, and reads St[buf] (dQ) after it.  The next writes of Q/dO[buf]
   // (swrite of slice it+1) and of St[buf] (slice it+2) both come after a later barrier
   // that every wave reaches only once it is done reading them.
-  for (int it = 0; it < total; ++it) {
-    const int buf = it & 1;
+  // The slice body is instantiated for buffer 0 and 1 (loop unrolled by two), so every LDS
+  // address is a lane-constant base plus an immediate offset.
+  auto slice = [&](const int it, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
     const int hq = hk * rep + it / iters_per_head;
     const int qbase = (qi0 + it % iters_per_head) * BMQ;
     if (it + 1 < total) gload(it + 1);
@@ -656,30 +662,36 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
     for (int qb = 0; qb < QB; ++qb) {
       const int q0 = qbase + 32 * qb;
       if (CAUSAL && q0 + 31 + off < kw0) continue;  // block fully masked: never read by dQ
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        const int oq = loff<D>(32 * qb + l32, ks * 16 + 8 * h32);
-        s = mfma32(lds_b128(Qc, oq), lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32)), s);
-        dp = mfma32(lds_b128(Dc, oq), vf[ks], dp);
-      }
-      const bool need_mask = (CAUSAL && (q0 + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
-                             (q0 + 32 > p.T);
+      // row constants as the initial accumulators: S - L/c and dP - delta come out of the
+      // MFMA chains ready for p = exp2(c s) and dS = p dp (no zero fill, no subtraction)
+      f32x16 s, dp;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const f32x4 L = *reinterpret_cast<const f32x4*>(lse_s + buf * BMQ + 32 * qb + 8 * g4 + 4 * h32);
         const f32x4 Dl = *reinterpret_cast<const f32x4*>(del_s + buf * BMQ + 32 * qb + 8 * g4 + 4 * h32);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g4 + j;
-          float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c, -L[j]));
-          if (need_mask) {
-            const int q = q0 + 8 * g4 + 4 * h32 + j;
-            if (mykey >= p.Tk || q >= p.T || (CAUSAL && mykey > q + off)) pv = 0.f;
-          }
-          s[r] = pv;
-          dp[r] = pv * (dp[r] - Dl[j]);  // dS / scale
+        for (int j = 0; j < 4; ++j) { s[4 * g4 + j] = L[j]; dp[4 * g4 + j] = Dl[j]; }
+      }
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const int oq = loff<D>(32 * qb + l32, ks * 16 + 8 * h32);
+        // K from registers under the causal mask (213 VGPRs); the non-causal build spills
+        // with both K and V resident, so it reads the K rows from the LDS image
+        const bf16x8 kfr = CAUSAL ? kf[ks] : lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
+        s = mfma32(lds_b128(Qc, oq), kfr, s);
+        dp = mfma32(lds_b128(Dc, oq), vf[ks], dp);
+      }
+      const bool need_mask = (CAUSAL && (q0 + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
+                             (q0 + 32 > p.T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = __builtin_amdgcn_exp2f(s[r] * c);
+        if (need_mask) {
+          const int q = q0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          if (mykey >= p.Tk || q >= p.T || (CAUSAL && mykey > q + off)) pv = 0.f;
         }
+        s[r] = pv;
+        dp[r] = pv * dp[r];  // dS / scale
       }
       bf16x8 pb[2], sb[2];
       pb[0] = acc_to_frag(s, 0);
@@ -736,6 +748,10 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
           }
       }
     }
+  };
+  for (int it = 0; it < total; it += 2) {
+    slice(it, std::integral_constant<int, 0>{});
+    if (it + 1 < total) slice(it + 1, std::integral_constant<int, 1>{});
   }
 
   // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
