@@ -519,17 +519,26 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_b
 // A 4-wave x 64-key form (one wave per SIMD) measured 1.07 ms vs 0.89 ms for the
 // 128-key kernel at B 64, T 1024, H 12, D 64 (latency-bound: 1.00 ms without atomics);
 // at D = 128 a 256-key form needs more than 512 registers, so D = 128 keeps v1.
-constexpr int BWD2_NW = 8, BWD2_BMQ = 64;
+constexpr int BWD2_NW = 8;
+template <int D>
+__host__ __device__ constexpr int bwd2_bmq() { return D == 64 ? 64 : 32; }
 
-// 8-byte-chunk (4 q) swizzle of the 128-byte dS^T image rows (bit permutation of k&15):
-// conflict-free ds_write_b64 of 16 consecutive keys, and the transposed reads of 4 rows at
-// 8-row spacing x 4 chunks per 16-lane group stay conflict-free per half-wave
+// 8-byte-chunk (4 q) swizzle of the dS^T image rows (BMQ q per row): conflict-free
+// ds_write_b64 of 16 consecutive keys, and conflict-free transposed reads of 4 rows at
+// 8-row spacing x 4 chunks per 16-lane group, per half-wave.  128-byte rows (BMQ 64): a
+// bit permutation of k&15; 64-byte rows (BMQ 32): (k>>1)&7.
+template <int BMQ>
 ORION_DEVICE int st_sw(int k) {
-  return (k & 1) | (((k >> 2) & 1) << 1) | (((k >> 3) & 1) << 2) | (((k >> 1) & 1) << 3);
+  if constexpr (BMQ == 64) {
+    return (k & 1) | (((k >> 2) & 1) << 1) | (((k >> 3) & 1) << 2) | (((k >> 1) & 1) << 3);
+  } else {
+    return (k >> 1) & 7;
+  }
 }
-// element offset of (key row k, q) in the [256][64] dS^T image
+// element offset of (key row k, q) in the [256][BMQ] dS^T image
+template <int BMQ>
 ORION_DEVICE int st_off(int k, int q) {
-  return k * BWD2_BMQ + 4 * ((q >> 2) ^ st_sw(k)) + (q & 3);
+  return k * BMQ + 4 * ((q >> 2) ^ st_sw<BMQ>(k)) + (q & 3);
 }
 
 ORION_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -539,7 +548,7 @@ ORION_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p) {
-  constexpr int NW = BWD2_NW, NT = NW * 64, BNK = 256, BMQ = BWD2_BMQ, QB = BMQ / 32;
+  constexpr int NW = BWD2_NW, NT = NW * 64, BNK = 256, BMQ = bwd2_bmq<D>(), QB = BMQ / 32;
   constexpr int NDB = D / 32, NCH = D / 8;
   constexpr int KT = BNK * D;     // K image elements
   constexpr int QT = BMQ * D;     // Q / dO slice elements
@@ -547,6 +556,7 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
   constexpr int NQC = BMQ * NCH;  // 16-byte chunks per Q (or dO) slice
   constexpr int NSTQ = 2 * NQC / NT;
   constexpr int D16 = D / 16;                       // 16-wide d blocks of dQ
+  constexpr bool KREG = CAUSAL && D == 64;          // K fragments in registers
   constexpr int TPW = (BMQ / 16) * D16 / NW;        // 16x16 dQ tiles per wave
   static_assert(BNK == NW * 32, "one 32-key block per wave");
   static_assert(TPW >= 1 && TPW * NW == (BMQ / 16) * D16, "dQ tiles must divide over the waves");
@@ -580,7 +590,7 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
     const long key = min(mykey, p.Tk - 1);
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
-      if (CAUSAL) kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
+      if (KREG) kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
       vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ks * 16 + 8 * h32);
     }
   }
@@ -675,11 +685,12 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
         const int oq = loff<D>(32 * qb + l32, ks * 16 + 8 * h32);
-        // K from registers under the causal mask (213 VGPRs); the non-causal build spills
-        // with both K and V resident, so it reads the K rows from the LDS image
-        const bf16x8 kfr = CAUSAL ? kf[ks] : lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
+        // K from registers only where they fit (D = 64, causal), else from the LDS image
+        const bf16x8 kfr = KREG ? kf[ks] : lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
         s = mfma32(lds_b128(Qc, oq), kfr, s);
         dp = mfma32(lds_b128(Dc, oq), vf[ks], dp);
+        // D = 128: cap how far the scheduler hoists fragment reads (register pressure)
+        if constexpr (D == 128) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
       }
       const bool need_mask = (CAUSAL && (q0 + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
                              (q0 + 32 > p.T);
@@ -699,19 +710,21 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
       sb[0] = acc_to_frag(dp, 0);
       sb[1] = acc_to_frag(dp, 1);
 #pragma unroll
-      for (int db = 0; db < NDB; ++db)
+      for (int db = 0; db < NDB; ++db) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           dva[db] = mfma32(tr_frag<D>(Dc, 32 * qb + 16 * s2 + 4 * h32, db * 32, lane, 8), pb[s2], dva[db]);
           dka[db] = mfma32(tr_frag<D>(Qc, 32 * qb + 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
         }
+        if constexpr (D == 128) __builtin_amdgcn_sched_barrier(0);
+      }
       // dS^T rows of the wave's 32 keys: registers 4g4..4g4+3 are q = 8 g4 + 4 h32 + 0..3
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         bf16x4 v4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v4[j] = sb[g4 >> 1][4 * (g4 & 1) + j];
-        *reinterpret_cast<bf16x4*>(Sc + st_off(wv * 32 + l32, 32 * qb + 8 * g4 + 4 * h32)) = v4;
+        *reinterpret_cast<bf16x4*>(Sc + st_off<BMQ>(wv * 32 + l32, 32 * qb + 8 * g4 + 4 * h32)) = v4;
       }
     }
     if (it + 1 < total) swrite(buf ^ 1);
@@ -733,7 +746,7 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
           const int qcol = 16 * (qgw * TPW + t) + 4 * (i & 3);
-          const bf16x8 a = cat8(lds_tr(Sc, st_off(kr, qcol)), lds_tr(Sc, st_off(kr + 4, qcol)));
+          const bf16x8 a = cat8(lds_tr(Sc, st_off<BMQ>(kr, qcol)), lds_tr(Sc, st_off<BMQ>(kr + 4, qcol)));
           dq[t] = mfma16(a, bk, dq[t]);
         }
       }
@@ -808,7 +821,7 @@ static size_t bwd_lds(int D) {
 }
 
 static size_t bwd2_lds(int D) {
-  const size_t bmq = BWD2_BMQ;
+  const size_t bmq = D == 64 ? bwd2_bmq<64>() : bwd2_bmq<128>();
   return (size_t)512 * D + 8 * bmq * D + 1024 * bmq + 16 * bmq;
 }
 
@@ -820,9 +833,9 @@ static void set_lds_attr() {
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)fwd_lds(D));
     hipFuncSetAttribute((const void*)attn_bwd_kernel<D, CAUSAL>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds(D));
-    if (D == 64)
-      hipFuncSetAttribute((const void*)attn_bwd2_kernel<64, CAUSAL>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd2_lds(64));
+    if constexpr (D == 64)
+      hipFuncSetAttribute((const void*)attn_bwd2_kernel<D, CAUSAL>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd2_lds(D));
     done = true;
   }
 }
@@ -863,7 +876,9 @@ int orion_attn_bwd(const AttnParams& p, int D, bool causal, float* delta, hipStr
   else return -1;
   AttnParams q = p;
   q.delta = delta;
-  if (bwd_v2() && D == 64) {  // D = 128: the 256-key form needs > 512 registers (spills)
+  // D = 128 stays on v1: the 8-wave form needs ~370 registers per lane there (110 spilled
+  // at the 256-register cap of two waves per SIMD) and the 4-wave form more than 512
+  if (bwd_v2() && D == 64) {
 #define BWD2(DD, CC)                                                                \
   set_lds_attr<DD, CC>();                                                           \
   attn_bwd2_kernel<DD, CC><<<((p.Tk + 255) / 256) * p.B * p.Hkv, BWD2_NW * 64, bwd2_lds(DD), st>>>(q);

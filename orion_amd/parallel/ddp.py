@@ -57,7 +57,9 @@ class GradBucketReducer:
             for s in slots:
                 self._slot_bucket[id(s.param)] = bi
         self._need = [len(sl) for (_, _, sl) in self.buckets]
-        self._count = [0] * len(self.buckets)
+        self._names = {id(s.param): s.name for s in arena.slots}
+        self._debug = None  # list -> (bucket, param, count, need) per arrival (tests)
+        self._arrived = [set() for _ in self.buckets]
         self._handles = [None] * len(self.buckets)
         self._sync = True
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._on_grad)
@@ -85,8 +87,16 @@ class GradBucketReducer:
         if not self._sync:
             return
         bi = self._slot_bucket[id(p)]
-        self._count[bi] += 1
-        if self._count[bi] == self._need[bi]:
+        # a parameter counts once per step: a weight whose GEMM wrote its gradient straight
+        # into the arena reports through its sink, and torch 2.10 still runs the (no-op)
+        # post-accumulate hook of that parameter afterwards
+        arrived = self._arrived[bi]
+        if id(p) in arrived:
+            return
+        arrived.add(id(p))
+        if self._debug is not None:
+            self._debug.append((bi, self._names[id(p)], len(arrived), self._need[bi]))
+        if len(arrived) == self._need[bi]:
             self._launch(bi)
 
     def _launch(self, bi):
@@ -110,7 +120,7 @@ class GradBucketReducer:
                 b0, b1, _ = self.buckets[bi]
                 self.arena.grads[b0:b1].div_(self.world)
         self._handles = [None] * len(self.buckets)
-        self._count = [0] * len(self.buckets)
+        self._arrived = [set() for _ in self.buckets]
 
     def remove(self):
         for h in self._hooks:
