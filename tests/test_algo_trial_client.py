@@ -178,6 +178,42 @@ def test_orion_compat_import():
     assert B is BaseAlgorithm
 
 
+# every module path of the reference's src/ tree, with the names it exported
+REFERENCE_PATHS = {
+    "orion.algo.base": ["BaseAlgorithm", "OptimizationAlgorithm"],
+    "orion.algo.random": ["Random"],
+    "orion.algo.space": ["Dimension", "Real", "Integer", "Categorical", "Space"],
+    "orion.algo.gradient_descent": ["Gradient_Descent"],
+    "orion.client": ["report_results"],
+    "orion.core": ["__version__", "DIRS"],
+    "orion.core.cli": ["main"],
+    "orion.core.resolve_config": ["fetch_orion_args", "fetch_default_options", "merge_env_vars",
+                                  "merge_orion_config", "ENV_VARS_DB"],
+    "orion.core.io.convert": ["Converter", "YAMLConverter", "JSONConverter",
+                              "infer_converter_from_file_type"],
+    "orion.core.io.space_builder": ["DimensionBuilder", "SpaceBuilder"],
+    "orion.core.io.database": ["AbstractDB", "Database", "DatabaseError", "DuplicateKeyError"],
+    "orion.core.io.database.mongodb": ["MongoDB"],
+    "orion.core.utils": ["SingletonType"],
+    "orion.core.utils.format_trials": ["trial_to_tuple", "tuple_to_trial", "get_trial_results"],
+    "orion.core.worker": ["workon"],
+    "orion.core.worker.consumer": ["Consumer"],
+    "orion.core.worker.producer": ["Producer"],
+    "orion.core.worker.experiment": ["Experiment"],
+    "orion.core.worker.primary_algo": ["PrimaryAlgo"],
+    "orion.core.worker.trial": ["Trial"],
+}
+
+
+@pytest.mark.parametrize("mod", sorted(REFERENCE_PATHS))
+def test_reference_module_paths(mod):
+    """A user of the reference finds every module path it had (src/orion/**), served by orion_amd."""
+    import importlib
+    m = importlib.import_module(mod)
+    for name in REFERENCE_PATHS[mod]:
+        assert hasattr(m, name), (mod, name)
+
+
 def test_converters(tmp_path):
     data = {"a": [1, 2, {"b": "x"}], "c": 1.5}
     for ext, klass in ((".yaml", YAMLConverter), (".yml", YAMLConverter), (".json", JSONConverter)):
