@@ -67,6 +67,15 @@ void check_bf16(const Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
 }
 
+// an optional in-place output: must be a contiguous bf16 vector of n elements
+bool has_out(const c10::optional<Tensor>& o, int64_t n, const char* name) {
+  if (!o.has_value() || !o->defined()) return false;
+  check_bf16(*o, name);
+  TORCH_CHECK(o->is_contiguous() && o->numel() == n, name, " must be contiguous with ", n,
+              " elements, got ", o->sizes());
+  return true;
+}
+
 // ------------------------------------------------------------------ layernorm
 std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& w,
                                                  const c10::optional<Tensor>& b, double eps) {
@@ -133,17 +142,24 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const
                                                          const Tensor& w, const Tensor& mean,
                                                          const Tensor& rstd, bool has_bias,
                                                          const c10::optional<Tensor>& dres,
-                                                         bool want_dx_colsum) {
+                                                         bool want_dx_colsum,
+                                                         const c10::optional<Tensor>& dw_out,
+                                                         const c10::optional<Tensor>& db_out,
+                                                         const c10::optional<Tensor>& dxs_out) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto dyc = dy.contiguous(), xc = x.contiguous();
   const int C = x.size(-1);
   const int rows = x.numel() / C;
   auto dx = at::empty_like(xc);
-  auto dw = at::empty({C}, w.options());
-  Tensor db = has_bias ? at::empty({C}, w.options()) : Tensor();
+  // a given *_out (a parameter's gradient-arena slice, ops/grad_sink.py) is written in place
+  // and its return slot is left undefined
+  const bool w_in = has_out(dw_out, C, "dw_out"), b_in = has_bias && has_out(db_out, C, "db_out");
+  const bool s_in = want_dx_colsum && has_out(dxs_out, C, "dxs_out");
+  Tensor dw = w_in ? *dw_out : at::empty({C}, w.options());
+  Tensor db = has_bias ? (b_in ? *db_out : at::empty({C}, w.options())) : Tensor();
   const int nb = orion_layernorm_bwd_blocks(rows);
   auto part = at::empty({3 * (long)nb * C + 48L * C}, x.options().dtype(at::kFloat));
-  Tensor dxs = want_dx_colsum ? at::empty({C}, x.options()) : Tensor();
+  Tensor dxs = want_dx_colsum ? (s_in ? *dxs_out : at::empty({C}, x.options())) : Tensor();
   Tensor drc;
   if (dres.has_value() && dres->defined()) {
     check_bf16(*dres, "dres");
@@ -155,7 +171,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const
                                    part.data_ptr<float>(), rows, C, drc.defined() ? drc.data_ptr() : nullptr,
                                    want_dx_colsum ? dxs.data_ptr() : nullptr, cur_stream()),
                "layernorm_bwd");
-  return {dx, dw, db, dxs};
+  return {dx, w_in ? Tensor() : dw, b_in ? Tensor() : db, s_in ? Tensor() : dxs};
 }
 
 // ------------------------------------------------------------------ activations
@@ -178,7 +194,8 @@ Tensor bias_gelu_fwd(const Tensor& x, const c10::optional<Tensor>& b) {
 }
 
 std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& x,
-                                         const c10::optional<Tensor>& b) {
+                                         const c10::optional<Tensor>& b,
+                                         const c10::optional<Tensor>& db_out) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto dyc = dy.contiguous(), xc = x.contiguous();
   const int C = x.size(-1);
@@ -191,8 +208,7 @@ std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& x,
   if (b.has_value() && b->defined()) {
     bc = b->contiguous();
     bp = bc.data_ptr();
-    db = at::empty({C}, b->options());
-    const int nb = orion_layernorm_bwd_blocks(rows);
+    db = has_out(db_out, C, "db_out") ? *db_out : at::empty({C}, b->options());
     partt = at::empty({(long)orion_colsum_scratch(rows, C)}, x.options().dtype(at::kFloat));
     part = partt.data_ptr<float>();
   }
@@ -205,16 +221,17 @@ std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& x,
                                         cur_stream()),
                  "colsum");
   }
-  return {dx, db};
+  return {dx, (db.defined() && has_out(db_out, C, "db_out")) ? Tensor() : db};
 }
 
-Tensor colsum(const Tensor& m) {
+Tensor colsum(const Tensor& m, const c10::optional<Tensor>& out_) {
   check_bf16(m, "m");
   c10::hip::HIPGuardMasqueradingAsCUDA g(m.device());
   auto mc = m.contiguous();
   const int C = m.size(-1);
   const int rows = m.numel() / C;
-  auto out = at::empty({C}, m.options());
+  const bool given = has_out(out_, C, "out");
+  auto out = given ? *out_ : at::empty({C}, m.options());
   auto part = at::empty({(long)orion_colsum_scratch(rows, C)}, m.options().dtype(at::kFloat));
   check_launch(orion_colsum_bf16(mc.data_ptr(), out.data_ptr(), part.data_ptr<float>(), rows, C,
                                  cur_stream()),
@@ -533,11 +550,11 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
 
 TORCH_LIBRARY(orion_amd, m) {
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias, Tensor? dres=None, bool want_dx_colsum=False) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias, Tensor? dres=None, bool want_dx_colsum=False, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, Tensor(c!)? dxs_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("add_layernorm_fwd(Tensor x, Tensor r, Tensor w, Tensor? b, float eps, Tensor? rbias=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor x, Tensor? b) -> Tensor");
-  m.def("bias_gelu_bwd(Tensor dy, Tensor x, Tensor? b) -> (Tensor, Tensor)");
-  m.def("colsum(Tensor m) -> Tensor");
+  m.def("bias_gelu_bwd(Tensor dy, Tensor x, Tensor? b, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");
+  m.def("colsum(Tensor m, Tensor(a!)? out=None) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gu) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");

@@ -4,6 +4,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
+from .layernorm import _claim, _notify, _unless, _view
 
 
 class _BiasGelu(torch.autograd.Function):
@@ -13,13 +14,17 @@ class _BiasGelu(torch.autograd.Function):
         y = C().bias_gelu_fwd(x, bb)
         ctx.save_for_backward(x, bb)
         ctx.b_dtype = None if b is None else b.dtype
+        ctx.bias = b
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x, bb = ctx.saved_tensors
-        dx, db = C().bias_gelu_bwd(dy.contiguous(), x, bb)
-        return dx.view(x.shape), (None if bb is None else db.to(ctx.b_dtype))
+        (sb,) = _claim((ctx.bias,))
+        dx, db = C().bias_gelu_bwd(dy.contiguous(), x, bb, _view(sb))
+        _notify(sb)
+        db = _unless(db, sb)
+        return dx.view(x.shape), (None if db is None else db.to(ctx.b_dtype))
 
 
 def bias_gelu_hip(x, bias):

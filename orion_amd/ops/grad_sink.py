@@ -67,3 +67,16 @@ def detach(param: torch.Tensor):
 def sink_of(param: torch.Tensor) -> GradSink | None:
     """The arena sink of ``param``, or None (not arena-owned, tied, or disabled)."""
     return getattr(param, "_orion_sink", None)
+
+
+def claim(param: torch.Tensor | None) -> GradSink | None:
+    """The sink of ``param`` if its gradient can be written straight into the arena by the
+    next kernel: only the first write of a step (it overwrites).  Later writes (gradient
+    accumulation) return the gradient and take the ``AccumulateGrad`` path instead.  The
+    caller passes ``sink.view`` as the kernel's output, then calls ``sink.notify()`` and
+    returns ``None`` for that gradient."""
+    sk = None if param is None else sink_of(param)
+    if sk is None or not sk.fresh:
+        return None
+    sk.fresh = False
+    return sk

@@ -7,11 +7,38 @@ import torch
 
 from ._ext import C
 from .gemm import wgrad, wgrad_into
-from .grad_sink import sink_of
+from .grad_sink import claim, sink_of
 
 
 def _bf16(t):
     return t if t is None or t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+
+
+# small gradients (norm weights, biases) go straight into their gradient-arena slices: the
+# reduction kernel's output IS the slice, so no AccumulateGrad add runs (ops/grad_sink.py)
+def _claim(params):
+    return tuple(claim(p) if p is not None and p.dtype == torch.bfloat16 else None
+                 for p in params)
+
+
+def _view(sink):
+    return None if sink is None else sink.view
+
+
+def _notify(*sinks):
+    for sk in sinks:
+        if sk is not None:
+            sk.notify()
+
+
+def _unless(g, sink):
+    # a gradient written through its sink must not also reach AccumulateGrad (the op may
+    # hand back the slice it wrote; ``p.grad += p.grad`` would double it)
+    return None if sink is not None else g
+
+
+def _grad(g, dtype):
+    return None if g is None else g.to(dtype)
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -23,15 +50,19 @@ class _LayerNorm(torch.autograd.Function):
         ctx.has_bias = b is not None
         ctx.b_dtype = None if b is None else b.dtype
         ctx.x_dtype = x.dtype
+        ctx.params = (w, b)
         return y.view(x.shape).to(x.dtype)
 
     @staticmethod
     def backward(ctx, dy):
         xb, w, mean, rstd = ctx.saved_tensors
+        sw, sb = _claim(ctx.params)
         dx, dw, db, _ = C().layernorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), mean, rstd,
-                                          ctx.has_bias)
+                                          ctx.has_bias, None, False, _view(sw), _view(sb))
+        _notify(sw, sb)
+        dw, db = _unless(dw, sw), _unless(db, sb)
         dx = dx.view(xb.shape).to(ctx.x_dtype)
-        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_bias else None), None
+        return dx, _grad(dw, w.dtype), (_grad(db, ctx.b_dtype) if ctx.has_bias else None), None
 
 
 def layer_norm_hip(x, weight, bias, eps=1e-5):
@@ -51,6 +82,7 @@ class _AddLayerNorm(torch.autograd.Function):
         ctx.has_bias = b is not None
         ctx.b_dtype = None if b is None else b.dtype
         ctx.rb_dtype = None if rb is None else rb.dtype
+        ctx.params = (w, b, rb)
         return s.view(x.shape), y.view(x.shape)
 
     @staticmethod
@@ -60,11 +92,15 @@ class _AddLayerNorm(torch.autograd.Function):
             dy = torch.zeros_like(s)
         dres = None if ds is None else ds.contiguous()
         want_rb = ctx.rb_dtype is not None
+        sw, sb, srb = _claim(ctx.params)
         dx, dw, db, drb = C().layernorm_bwd(dy.contiguous(), s, _bf16(w), mean, rstd,
-                                            ctx.has_bias, dres, want_rb)
+                                            ctx.has_bias, dres, want_rb, _view(sw), _view(sb),
+                                            _view(srb))
+        _notify(sw, sb, srb)
+        dw, db, drb = _unless(dw, sw), _unless(db, sb), _unless(drb, srb)
         dx = dx.view(s.shape)
-        return (dx, dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_bias else None),
-                (drb.to(ctx.rb_dtype) if want_rb else None), None)
+        return (dx, dx, _grad(dw, w.dtype), (_grad(db, ctx.b_dtype) if ctx.has_bias else None),
+                (_grad(drb, ctx.rb_dtype) if want_rb else None), None)
 
 
 def add_layer_norm_hip(x, r, weight, bias, eps=1e-5, r_bias=None):
@@ -80,6 +116,7 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         ctx.sink = sink_of(w)  # dW straight into the gradient arena (ops/grad_sink.py)
+        ctx.bias = b
         return torch.nn.functional.linear(x, w, b)
 
     @staticmethod
@@ -97,7 +134,11 @@ class _Linear(torch.autograd.Function):
             else:
                 dw = wgrad(dy2, x.reshape(-1, x.shape[-1]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = C().colsum(dy2.contiguous())
+            (sb,) = _claim((ctx.bias,))
+            db = C().colsum(dy2.contiguous(), _view(sb))
+            if sb is not None:  # written into the arena; never hand the slice back to autograd
+                db = None
+            _notify(sb)
         return dx, dw, db
 
 
