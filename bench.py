@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-tuned-gemms", action="store_true",
                     help="do not load the committed TunableOp GEMM table (orion_amd/tuning/)")
     ap.add_argument("--gemm-table", default=None, help="TunableOp table to load instead of the committed one")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, the real run) or gloo (rehearsing N>1 on one GPU)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the whole training step in a HIP graph (single GPU)")
     return ap.parse_args()
@@ -60,10 +62,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; a gloo rehearsal may put several ranks on one device
+    ordinal = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", ordinal))
+        else:
+            dist.init_process_group(args.dist_backend)
+    torch.cuda.set_device(ordinal)
+    dev = torch.device("cuda", ordinal)
     n_tuned = 0
     # TunableOp's table is not applied under HIP-graph capture (solutions chosen by index
     # went wrong on replay in testing); graph runs use hipBLASLt's default heuristics
@@ -101,7 +108,7 @@ def main():
     else:
         ddp_model = model
         if world > 1:
-            ddp_model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank],
+            ddp_model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[ordinal],
                                                                   bucket_cap_mb=args.bucket_mb)
         opt = torch.optim.AdamW(model.parameters(), lr=ocfg.learning_rate, betas=(0.9, 0.95),
                                 weight_decay=0.1, fused=True)
