@@ -14,6 +14,9 @@ Design (MI355X-first, not a translation of any NCCL call pattern):
   issued asynchronously (RCCL runs on its own HIP stream, ordered after the
   producing kernels by an event), so communication overlaps the rest of
   backward;
+* a tied parameter (GPT-2's ``wte`` = LM head) starts a bucket of its own: its
+  gradient is complete only after the embedding backward, the last kernel of the
+  pass, and would otherwise hold back every layer sharing its bucket;
 * gradient accumulation: reduction is only armed on the last micro-step
   (``set_sync``), the same contract as DDP's ``no_sync``.
 
@@ -39,7 +42,13 @@ class GradBucketReducer:
         cap = max(1, int(bucket_mb * 1024 * 1024 / esize))
         # bucket boundaries on parameter boundaries, in arena order
         buckets, cur, start = [], [], 0
+        shared = getattr(arena, "shared", set())
         for s in arena.slots:
+            # a shared (tied) parameter's gradient completes last: give it a bucket of its
+            # own so the layers before it are reduced while the embedding backward runs
+            if id(s.param) in shared and cur:
+                buckets.append((start, s.offset, cur))
+                cur, start = [], s.offset
             cur.append(s)
             end = s.offset + s.numel
             if end - start >= cap:

@@ -66,6 +66,9 @@ class FlatArena:
             off = _round_up(off + p.numel(), ALIGN)
         self.numel = off
         self.slots = slots
+        # parameters used by more than one module (GPT-2's wte / LM head): their gradient is
+        # complete only after the LAST use's backward (the embedding, at the very end)
+        self.shared = {id(p) for _, p in named if uses.get(id(p), 1) > 1}
         self.dtype = dtype
         self.device = device
         self.params = torch.zeros(off, dtype=dtype, device=device)

@@ -79,3 +79,24 @@ def test_ddp_matches_single_process(bucket_mb, accum):
         _, loss = model(x, y)
         (loss / (world * accum)).backward()
     assert torch.allclose(g0, arena.grads, atol=1e-6, rtol=1e-4)
+
+
+def test_tied_parameter_gets_its_own_bucket():
+    """GPT-2's wte (= LM head) completes only after the embedding backward: it must not hold
+    back the layers laid out next to it, so it starts a bucket of its own."""
+    from orion_amd.parallel.ddp import GradBucketReducer
+    from orion_amd.train.flat import FlatArena
+    port = _free_port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        arena = FlatArena(build_gpt2("gpt2-tiny", block_size=32))
+        red = GradBucketReducer(arena, bucket_mb=1000.0)  # one bucket but for the split
+        names = [[s.name for s in sl] for _, _, sl in red.buckets]
+        assert names[-1] == ["transformer.wte.weight"], names[-1]
+        assert len(red.buckets) == 2
+        covered = [b1 - b0 for b0, b1, _ in red.buckets]
+        assert sum(covered) == arena.numel and red.buckets[0][0] == 0
+        red.remove()
+    finally:
+        dist.destroy_process_group()
