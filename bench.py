@@ -6,12 +6,21 @@ launched by ``torch.distributed.run`` with one rank per GPU (RCCL over xGMI).
 W untimed warm-up optimizer steps, then exactly K timed optimizer steps
 bracketed by barrier + device synchronize; the elapsed time is the MAX over
 ranks; rank 0 prints one JSON line whose ``value`` is the whole-job token
-throughput (tokens/s summed over all GPUs).
+throughput (tokens/s summed over all GPUs); ``per_gpu`` is value / n_gpus, the
+tokens/sec/GPU of BASELINE.json's metric, and ``vs_baseline`` compares that per-GPU
+rate with the baseline's per-GPU figure.
 
 Every timed step is a complete training step: ``grad_accum`` micro-batches of
 forward + backward through the full 12-layer model, gradient all-reduce (N>1)
 and the fused AdamW update with global-norm clipping.  Data is synthetic
 (random token ids, fixed pool resident on the GPU), weights random-init.
+
+``--gpus N`` without ``WORLD_SIZE`` in the environment starts the N ranks itself
+(``orion_amd/parallel/launch.py``: one process per GPU, spawned before anything
+touches HIP), so ``python bench.py --gpus 8`` and the driver's
+``torch.distributed.run ... bench.py --gpus 8`` run the same RCCL job.  For N>1 the
+JSON also carries the RCCL all-reduce bus bandwidth of one gradient-arena-sized
+buffer, measured after the timed region.
 
 ``--impl torch`` runs the same model on stock PyTorch ops (SDPA, F.layer_norm,
 fp32 master params under bf16 autocast, fused torch AdamW) -- the nanoGPT
@@ -52,6 +61,9 @@ def parse():
     ap.add_argument("--gemm-table", default=None, help="TunableOp table to load instead of the committed one")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the real run) or gloo (rehearsing N>1 on one GPU)")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: plumbing rehearsal (reference ops, gloo) -- not a measurement")
+    ap.add_argument("--no-busbw", action="store_true", help="skip the post-run all-reduce probe")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the whole training step in a HIP graph (single GPU)")
     return ap.parse_args()
@@ -59,22 +71,28 @@ def parse():
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU; a gloo rehearsal may put several ranks on one device
-    ordinal = local_rank % max(1, torch.cuda.device_count())
+    from orion_amd.parallel import launch
+    if args.gpus > 1 and not launch.in_launched_job():
+        # spawn the ranks before this process touches the GPU; exit with the job's status
+        sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    world, rank, local_rank = launch.check_world(args.gpus)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if args.device == "cpu":
+        if args.dist_backend == "nccl":
+            args.dist_backend = "gloo"
+        dev = torch.device("cpu")
+    else:
+        dev = launch.device_for(local_rank, local_world, args.dist_backend)
+        torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", ordinal))
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
-    torch.cuda.set_device(ordinal)
-    dev = torch.device("cuda", ordinal)
     n_tuned = 0
     # TunableOp's table is not applied under HIP-graph capture (solutions chosen by index
     # went wrong on replay in testing); graph runs use hipBLASLt's default heuristics
-    if not args.no_tuned_gemms and not args.hip_graph:
+    if dev.type == "cuda" and not args.no_tuned_gemms and not args.hip_graph:
         from orion_amd.tuning import use_tuned_gemms
         n_tuned = use_tuned_gemms(args.gemm_table, verbose=(rank == 0))
     torch.manual_seed(1337 + rank)
@@ -85,7 +103,7 @@ def main():
 
     if args.impl == "torch":
         ops.set_backend("torch")
-    else:
+    elif dev.type == "cuda":
         ops.load_ext(required=True)
 
     is_gpt2 = args.model in GPT2_PRESETS
@@ -108,7 +126,8 @@ def main():
     else:
         ddp_model = model
         if world > 1:
-            ddp_model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[ordinal],
+            ddp_model = torch.nn.parallel.DistributedDataParallel(
+                model, device_ids=[dev.index] if dev.type == "cuda" else None,
                                                                   bucket_cap_mb=args.bucket_mb)
         opt = torch.optim.AdamW(model.parameters(), lr=ocfg.learning_rate, betas=(0.9, 0.95),
                                 weight_decay=0.1, fused=True)
@@ -119,7 +138,7 @@ def main():
             for j in range(A):
                 x, y = pool[(i * A + j) % 4]
                 ctx = ddp_model.no_sync() if (world > 1 and j < A - 1) else _null()
-                with ctx, torch.autocast("cuda", dtype=torch.bfloat16):
+                with ctx, torch.autocast(dev.type, dtype=torch.bfloat16):
                     _, loss = ddp_model(x, y)
                 (loss / A).backward()
                 tot = tot + loss.detach()
@@ -131,39 +150,50 @@ def main():
         if world > 1:
             dist.barrier()
 
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
     loss = None
     trace = os.environ.get("ORION_BENCH_TRACE_LOSS") == "1"  # debugging: per-step loss (syncs)
     for i in range(args.warmup):
         loss = step_fn(i)
         if trace:
             print(f"warmup {i} loss {float(loss):.4f}", file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step_fn(args.warmup + i)
         if trace:
             print(f"step {i} loss {float(loss):.4f}", file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     final_loss = float(loss)
+    busbw = None
+    if world > 1 and not args.no_busbw and args.impl == "native":
+        from orion_amd.parallel.busbw import allreduce_busbw
+        busbw = allreduce_busbw(trainer.arena.grads, iters=5)
 
     tokens = world * B * T * A * args.steps
     tok_s = tokens / elapsed
     flops_tok = model.flops_per_token(T)
     mfu = tok_s / world * flops_tok / 2.5e15
+    headline = args.model == "gpt2" and T == 1024 and dev.type == "cuda"
     if rank == 0:
         out = {
-            "metric": ("tokens/sec/GPU, GPT-2-124M bf16 seq=1024, at 1/2/4/8 MI355X"
-                       if args.model == "gpt2" and T == 1024 else
-                       f"tokens/sec/GPU, {args.model} bf16 seq={T} (secondary config)"),
+            # BASELINE.json's metric is tokens/sec/GPU at 1/2/4/8 GPUs: ``value`` is the whole
+            # job's rate (the driver's contract), ``per_gpu`` = value / n_gpus is that metric
+            "metric": ("tokens/sec (whole job; per_gpu = tokens/sec/GPU), GPT-2-124M bf16 seq=1024, "
+                       "at 1/2/4/8 MI355X" if headline else
+                       f"tokens/sec (whole job), {args.model} bf16 seq={T} on {dev.type} (secondary config)"),
             "value": round(tok_s, 1),
             "unit": "tokens/s (whole job, summed over n_gpus)",
             "n_gpus": world,
@@ -172,18 +202,22 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1000, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(tok_s / (BASELINE_TOK_S_PER_GPU * world), 3)
-                            if args.model == "gpt2" and T == 1024 else None),
-            "baseline": "1.07e5 tokens/s per GPU (BASELINE.md, nanoGPT 8xA100 derived) x n_gpus",
+            "vs_baseline": round(tok_s / world / BASELINE_TOK_S_PER_GPU, 3) if headline else None,
+            "baseline": "1.07e5 tokens/s per GPU (BASELINE.md, nanoGPT 8xA100 derived); "
+                        "vs_baseline = per_gpu / 1.07e5",
             "per_gpu": round(tok_s / world, 1),
             "dtype": "bf16",
             "data": "synthetic (random token ids), random-init weights",
             "impl": args.impl,
             "tuned_gemm_entries": n_tuned,
             "hip_graph": bool(args.impl == "native" and trainer.graph_enabled),
+            "grad_dtype": str(trainer.arena.grads.dtype).replace("torch.", "") if args.impl == "native" else None,
             "mfu_vs_2.5PF_dense_bf16": round(mfu, 4),
             "loss": round(final_loss, 4),
-            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
+            "max_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+                           if dev.type == "cuda" else None),
+            "dist_backend": args.dist_backend if world > 1 else None,
+            "allreduce_busbw_gbps": busbw,
             "config": {"model": f"{args.model} ({n_params / 1e6:.1f}M params)",
                        "global_batch": B * A * world, "micro_batch": B, "grad_accum": A,
                        "seq_len": T, "tokens_per_step": B * T * A * world,

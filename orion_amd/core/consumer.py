@@ -13,7 +13,11 @@ MI355X-node additions:
   ``HIP_VISIBLE_DEVICES``; k > 1 trials of a Python script are launched through
   ``torch.distributed.run --standalone --nproc-per-node k`` (one rank per GPU,
   RCCL over xGMI);
-* liveness: while the child runs, the trial's ``heartbeat`` is refreshed;
+* liveness: from reservation on -- while the trial waits for its GPU lease and
+  while the child runs -- the trial's ``heartbeat`` is refreshed; if a refresh finds
+  the trial no longer ``reserved`` (a reaper re-queued it because this worker
+  looked dead), the child is stopped and the trial is abandoned without writing
+  anything, so no trial is ever completed twice;
 * ``trial_timeout``: the child is killed and the trial marked ``broken``;
 * SIGINT/SIGTERM of the worker: the child is terminated and the trial is
   returned to the pool as ``interrupted`` (the reference had the status but
@@ -41,6 +45,10 @@ class TrialInterrupted(Exception):
     pass
 
 
+class TrialLost(Exception):
+    """The reservation was taken away (stale heartbeat re-queued by another worker)."""
+
+
 class Consumer:
     def __init__(self, experiment, gpu_pool=None, gpus_per_trial=0, heartbeat=30.0,
                  trial_timeout=None, worker_id=None):
@@ -49,7 +57,7 @@ class Consumer:
         if self.space is None:
             raise RuntimeError("Experiment object provided to Consumer has not yet completed "
                                "initialization.")
-        self.template_builder = experiment.space_builder
+        self.template = experiment.template
         self.script_path = experiment.metadata["user_script"]
         self.tmp_dir = os.path.join(tempfile.gettempdir(), "orion")
         os.makedirs(self.tmp_dir, exist_ok=True)
@@ -72,11 +80,17 @@ class Consumer:
                 log.warning("worker interrupted: trial %s -> interrupted", trial.id)
                 self.experiment.set_trial_status(trial, "interrupted", only_if="reserved")
                 raise KeyboardInterrupt
+            except TrialLost:
+                log.warning("trial %s was re-queued while this worker held it; abandoning it",
+                            trial.id)
+                return "lost"
         if done is not None:
-            self.experiment.push_completed_trial(done)
+            if not self.experiment.push_completed_trial(done, only_if_reserved=True):
+                log.warning("trial %s is no longer reserved by this worker; result dropped", trial.id)
+                return "lost"
             return "completed"
         log.debug("### Save %s as broken.", trial)
-        self.experiment.set_trial_status(trial, "broken")
+        self.experiment.set_trial_status(trial, "broken", only_if="reserved")
         return "broken"
 
     # ------------------------------------------------------------------ internals
@@ -87,10 +101,11 @@ class Consumer:
         res = tempfile.NamedTemporaryFile(mode="w", prefix="results_", suffix=".log", dir=workdir,
                                           delete=False)
         res.close()
-        cmd_args = self.template_builder.build_to(conf.name, trial)
+        cmd_args = self.template.render(trial, conf.name)
+        self._last_beat = time.monotonic()
         lease = None
         if self.gpus_per_trial:
-            lease = self.gpu_pool.acquire(self.gpus_per_trial)
+            lease = self._acquire_lease(trial)
         try:
             rc = self._run(res.name, cmd_args, trial, lease)
         finally:
@@ -115,8 +130,29 @@ class Consumer:
         return trial
 
     def _conf_suffix(self):
-        cfg = getattr(self.template_builder, "userconfig", None)
+        cfg = self.template.config_path
         return os.path.splitext(cfg)[1] if cfg else ".conf"
+
+    def _beat(self, trial, force=False):
+        """Refresh the trial's heartbeat every ``self.heartbeat`` seconds; raise
+        :class:`TrialLost` when the trial is no longer ours."""
+        now = time.monotonic()
+        if force or now - self._last_beat >= self.heartbeat:
+            self._last_beat = now
+            if not self.experiment.update_heartbeat(trial):
+                raise TrialLost(trial.id)
+
+    def _acquire_lease(self, trial, poll=0.5):
+        """Wait for ``gpus_per_trial`` devices while keeping the reservation alive."""
+        if self.gpus_per_trial > len(self.gpu_pool.gpu_ids):
+            raise RuntimeError(f"trial needs {self.gpus_per_trial} GPUs but only "
+                               f"{len(self.gpu_pool.gpu_ids)} are visible")
+        while True:
+            lease = self.gpu_pool.try_acquire(self.gpus_per_trial)
+            if lease is not None:
+                return lease
+            self._beat(trial)
+            time.sleep(min(poll, self.heartbeat))
 
     def command(self, cmd_args):
         script = self.script_path
@@ -177,9 +213,11 @@ class Consumer:
                     log.error("trial %s exceeded its %ss timeout", trial.id, self.trial_timeout)
                     self._kill(proc)
                     return -9
-                if time.monotonic() - getattr(self, "_last_beat", 0.0) >= self.heartbeat:
-                    self._last_beat = time.monotonic()
-                    self.experiment.update_heartbeat(trial)
+                try:
+                    self._beat(trial)
+                except TrialLost:
+                    self._kill(proc)
+                    raise
         finally:
             for s, h in prev.items():
                 signal.signal(s, h)

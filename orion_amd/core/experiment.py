@@ -12,8 +12,11 @@ algorithm declares itself done; ``stats`` summarises it.
 
 Deliberate fixes of reference quirks:
 
-* explicit storage handle and the experiment owns its :class:`SpaceBuilder`
-  (templates) instead of process singletons (items 1);
+* explicit storage handle, and the experiment owns its immutable
+  :class:`~orion_amd.space.dsl.ScriptTemplate` instead of process singletons
+  (item 1); configuration planning is a pure function (:func:`plan_configuration`);
+* ``is_done`` is a side-effect-free query; :meth:`Experiment.finish_if_done` records
+  the ``done`` status (item 3);
 * ``stats`` works with zero completed trials (item 2);
 * bounded reservation retry loop instead of unbounded recursion (item 6);
 * incremental fetch keeps a set of already-observed trial ids and re-reads a
@@ -30,8 +33,9 @@ import datetime
 import getpass
 import logging
 import random
+from dataclasses import dataclass
 
-from ..space.dsl import SpaceBuilder
+from ..space.dsl import ScriptTemplate
 from ..store import DuplicateKeyError
 from .format_trials import trial_to_tuple
 from .primary_algo import PrimaryAlgo
@@ -51,7 +55,7 @@ def utcnow():
 
 class Experiment:
     __slots__ = ("name", "refers", "metadata", "pool_size", "max_trials", "status", "algorithms",
-                 "_db", "_init_done", "_id", "_last_fetched", "_seen", "space_builder", "_user")
+                 "_db", "_init_done", "_id", "_last_fetched", "_seen", "template", "_user")
     non_forking_attrs = ("status", "pool_size", "max_trials")
     _config_attrs = ("name", "refers", "metadata", "pool_size", "max_trials", "status", "algorithms")
     MAX_RESERVE_ATTEMPTS = 64
@@ -69,7 +73,7 @@ class Experiment:
         self.max_trials = None
         self.status = None
         self.algorithms = None
-        self.space_builder = None
+        self.template = None
         self._seen = set()
         docs = self._db.read("experiments", {"name": name, "metadata.user": self._user})
         if docs:
@@ -140,10 +144,22 @@ class Experiment:
             for t, d in zip(trials, docs):
                 t._id = d["_id"]
 
-    def push_completed_trial(self, trial):
+    def push_completed_trial(self, trial, only_if_reserved=False):
+        """Store ``trial`` as completed.  With ``only_if_reserved`` the write is a
+        compare-and-swap on ``status='reserved'`` (and on the reserving worker when the
+        trial carries one): a trial that was re-queued meanwhile is not overwritten.
+        Returns whether the trial was written."""
         trial.end_time = utcnow()
         trial.status = "completed"
-        self._db.write("trials", trial.to_dict(), query={"_id": trial.id})
+        doc = trial.to_dict()
+        if not only_if_reserved:
+            self._db.write("trials", doc, query={"_id": trial.id})
+            return True
+        q = {"_id": trial.id, "status": "reserved"}
+        if getattr(trial, "worker", None) is not None:
+            q["worker"] = trial.worker
+        doc.pop("_id", None)
+        return self._db.read_and_write("trials", q, doc) is not None
 
     def set_trial_status(self, trial, status, only_if=None):
         """Move ``trial`` to ``status``; with ``only_if`` it is a CAS on the current status."""
@@ -198,18 +214,34 @@ class Experiment:
         return self._db.count("trials", q)
 
     # ------------------------------------------------------------------ state
+    def _finished(self):
+        n_completed = self.count_trials("completed")
+        return n_completed >= self.max_trials or bool(self._init_done and self.algorithms.is_done)
+
     @property
     def is_done(self):
-        n_completed = self.count_trials("completed")
-        if n_completed >= self.max_trials or (self._init_done and self.algorithms.is_done):
+        """True when ``max_trials`` trials completed or the algorithm declares itself done.
+        Pure query: recording ``status='done'`` is :meth:`finish_if_done`'s job (the
+        reference's property wrote to the database)."""
+        return self._finished()
+
+    def finish_if_done(self):
+        """:attr:`is_done`, and if so persist ``status='done'`` once."""
+        if not self._finished():
+            return False
+        if self.status != "done":
             self._db.write("experiments", {"status": "done"}, {"_id": self._id})
             self.status = "done"
-            return True
-        return False
+        return True
 
     @property
     def space(self):
         return self.algorithms.space if self._init_done else None
+
+    @property
+    def space_builder(self):
+        """The experiment's :class:`ScriptTemplate` (kept under the old attribute name)."""
+        return self.template
 
     @property
     def configuration(self):
@@ -222,73 +254,35 @@ class Experiment:
         return copy.deepcopy(cfg)
 
     def configure(self, config):
-        """Create (new name) or resume (existing, same configuration) the experiment."""
+        """Create (unknown ``(name, user)``) or resume (stored, same identity) the experiment.
+
+        The work is split into a pure planning step, :func:`plan_configuration`, which
+        overlays ``config`` on the stored document, normalises it by instantiating the
+        template and the algorithm, and rejects a changed identity (a "fork"); and the
+        adoption + single database write here."""
         if self._init_done:
             raise RuntimeError("Configuration is done; cannot reset an Experiment.")
-        shadow = Experiment(self.name, self._db, user=self._user)
-        shadow._instantiate_config(self.configuration)
-        shadow._instantiate_config(config)
-        shadow._init_done = True
-        shadow.status = "pending"
-        if self.status is None:
-            if config["name"] != self.name or \
-                    config["metadata"]["user"] != self.metadata["user"] or \
-                    config["metadata"]["datetime"] != self.metadata["datetime"]:
+        creating = self.status is None
+        if creating:
+            md = config.get("metadata") or {}
+            if (config.get("name"), md.get("user"), md.get("datetime")) != \
+                    (self.name, self.metadata["user"], self.metadata["datetime"]):
                 raise ValueError("Configuration given is inconsistent with this Experiment.")
-            is_new = True
-        else:
-            is_new = self._is_different_from(shadow.configuration)
-            if is_new:
-                self._fork_config(config)
-        final = shadow.configuration
-        self._instantiate_config(final)
-        self._init_done = True
+        plan = plan_configuration(None if creating else self.configuration, config)
+        for attr in self._config_attrs:
+            setattr(self, attr, plan.config.get(attr))
+        self.template = plan.template
+        if plan.algorithms is not None:
+            self.algorithms = plan.algorithms
+        self._init_done = plan.algorithms is not None
         self.status = "pending"
-        if is_new:
-            self._db.write("experiments", final)  # DuplicateKeyError on a creation race
-            self._id = final["_id"]
+        if creating:
+            doc = plan.config
+            self._db.write("experiments", doc)  # DuplicateKeyError on a creation race
+            self._id = doc["_id"]
         else:
-            final.pop("name")
-            self._db.write("experiments", final, {"_id": self._id})
-
-    def _instantiate_config(self, config):
-        for section, value in config.items():
-            if section == "status":
-                continue
-            if section not in self._config_attrs:
-                log.warning("Found section '%s' in configuration. Experiments do not support "
-                            "this option. Ignoring.", section)
-                continue
-            setattr(self, section, value)
-        try:
-            builder = SpaceBuilder()
-            space = builder.build_from(config["metadata"]["user_args"])
-            if not space:
-                raise ValueError("Parameter space is empty. There is nothing to optimize.")
-            self.space_builder = builder
-            self.algorithms = PrimaryAlgo(space, self.algorithms)
-        except KeyError:
-            pass
-
-    def _fork_config(self, config):
-        raise NotImplementedError(
-            f"Experiment '{self.name}' exists with a different configuration; forking is not "
-            "supported -- use a new experiment name (-n).")
-
-    def _is_different_from(self, config):
-        for section, value in config.items():
-            if section in self.non_forking_attrs or section not in self._config_attrs:
-                continue
-            item = getattr(self, section)
-            if section == "metadata":
-                item = {k: v for k, v in (item or {}).items() if k not in ("datetime", "orion_version")}
-                value = {k: v for k, v in (value or {}).items() if k not in ("datetime", "orion_version")}
-            if item != value:
-                log.warning("Config given is different from config found in db at section: %s", section)
-                log.warning("Config+ :\n%s", value)
-                log.warning("Config- :\n%s", item)
-                return True
-        return False
+            self._db.write("experiments", {k: v for k, v in plan.config.items() if k != "name"},
+                           {"_id": self._id})
 
     # ------------------------------------------------------------------ stats
     @property
@@ -335,3 +329,64 @@ def create_experiment(name, storage, config, user=None, _retry=True):
             raise
         return create_experiment(name, storage, config, user=user, _retry=False)
     return exp
+
+
+# ---------------------------------------------------------------------------- configuration
+CONFIG_ATTRS = Experiment._config_attrs
+# sections that may change when an experiment is resumed
+MUTABLE_SECTIONS = Experiment.non_forking_attrs
+# metadata keys that do not identify an experiment
+VOLATILE_METADATA = ("datetime", "orion_version")
+
+
+@dataclass
+class ConfigPlan:
+    config: dict            # the document to store (algorithms normalised)
+    template: object        # ScriptTemplate or None (no user_args yet)
+    algorithms: object      # PrimaryAlgo or None
+
+
+def _identity(cfg: dict) -> dict:
+    """The sections that define WHAT an experiment optimises."""
+    ident = {}
+    for k in CONFIG_ATTRS:
+        if k in MUTABLE_SECTIONS:
+            continue
+        v = cfg.get(k)
+        if k == "metadata":
+            v = {mk: mv for mk, mv in (v or {}).items() if mk not in VOLATILE_METADATA}
+        ident[k] = v
+    return ident
+
+
+def plan_configuration(stored: dict | None, requested: dict) -> ConfigPlan:
+    """Overlay ``requested`` on ``stored`` (None: a new experiment), instantiate the
+    script template and the algorithm to normalise the algorithm section, and refuse a
+    resume whose identity differs from the stored one.  No side effects on any store."""
+    for k in requested:
+        if k not in CONFIG_ATTRS:
+            log.warning("Found section '%s' in configuration. Experiments do not support "
+                        "this option. Ignoring.", k)
+    cfg = {k: copy.deepcopy(requested[k] if k in requested else (stored or {}).get(k))
+           for k in CONFIG_ATTRS}
+    cfg["status"] = "pending"
+    template = algorithms = None
+    user_args = (cfg.get("metadata") or {}).get("user_args")
+    if user_args is not None:
+        template = ScriptTemplate.parse(user_args)
+        if not template.space:
+            raise ValueError("Parameter space is empty. There is nothing to optimize.")
+        algorithms = PrimaryAlgo(template.space, cfg.get("algorithms"))
+        cfg["algorithms"] = algorithms.configuration
+    if stored is not None:
+        old, new = _identity(stored), _identity(cfg)
+        changed = [k for k in old if old[k] != new[k]]
+        if changed:
+            for k in changed:
+                log.warning("Config given is different from config found in db at section: %s\n"
+                            "  stored:    %s\n  requested: %s", k, old[k], new[k])
+            raise NotImplementedError(
+                f"Experiment '{cfg.get('name')}' exists with a different configuration "
+                f"({', '.join(changed)}); forking is not supported -- use a new experiment "
+                "name (-n).")
+    return ConfigPlan(cfg, template, algorithms)

@@ -39,7 +39,7 @@ def workon(experiment, gpus_per_trial=0, heartbeat=30.0, trial_timeout=None, max
         trial = experiment.reserve_trial(score_handle=producer.algorithm.score, worker=worker_id)
         if trial is None:
             producer.update()
-            if experiment.is_done:
+            if experiment.finish_if_done():
                 break
             experiment.fix_lost_trials(stale_after)
             if experiment.count_trials(("new", "suspended", "interrupted")) == 0:

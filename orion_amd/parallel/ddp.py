@@ -10,10 +10,15 @@ Design (MI355X-first, not a translation of any NCCL call pattern):
   needs tens of MB per call to spread its channels over all links; fewer,
   larger collectives also mean fewer launches competing with backward;
 * a ``register_post_accumulate_grad_hook`` per parameter counts arrivals per
-  bucket; the moment a bucket's last gradient lands its ``all_reduce`` is
-  issued asynchronously (RCCL runs on its own HIP stream, ordered after the
-  producing kernels by an event), so communication overlaps the rest of
-  backward;
+  bucket; once a bucket's last gradient lands its ``all_reduce`` is issued
+  asynchronously (RCCL runs on its own HIP stream, ordered after the producing
+  kernels by an event), so communication overlaps the rest of backward;
+* collectives are issued strictly in bucket order: bucket i launches only after
+  buckets 0..i-1 have.  RCCL matches collectives by issue order on every rank,
+  and gradient ARRIVAL order is not guaranteed to agree across ranks (sink
+  notifications vs AccumulateGrad hooks, unused parameters, data-dependent
+  graphs); a ready bucket behind a not-yet-ready one waits in ``_ready`` and is
+  flushed the moment the cursor reaches it;
 * a tied parameter (GPT-2's ``wte`` = LM head) starts a bucket of its own: its
   gradient is complete only after the embedding backward, the last kernel of the
   pass, and would otherwise hold back every layer sharing its bucket;
@@ -70,6 +75,9 @@ class GradBucketReducer:
         self._debug = None  # list -> (bucket, param, count, need) per arrival (tests)
         self._arrived = [set() for _ in self.buckets]
         self._handles = [None] * len(self.buckets)
+        self._ready = [False] * len(self.buckets)
+        self._cursor = 0                 # next bucket index allowed to launch
+        self.launch_log: list[int] | None = None  # tests: bucket indices in launch order
         self._sync = True
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._on_grad)
                        for s in arena.slots]
@@ -106,11 +114,20 @@ class GradBucketReducer:
         if self._debug is not None:
             self._debug.append((bi, self._names[id(p)], len(arrived), self._need[bi]))
         if len(arrived) == self._need[bi]:
-            self._launch(bi)
+            self._ready[bi] = True
+            self._flush()
+
+    def _flush(self):
+        """Launch every ready bucket at the cursor, in index order."""
+        while self._cursor < len(self.buckets) and self._ready[self._cursor]:
+            self._launch(self._cursor)
+            self._cursor += 1
 
     def _launch(self, bi):
         if self._handles[bi] is not None:
             return
+        if self.launch_log is not None:
+            self.launch_log.append(bi)
         b0, b1, _ = self.buckets[bi]
         view = self.arena.grads[b0:b1]
         op = dist.ReduceOp.AVG if self._use_avg_op else dist.ReduceOp.SUM
@@ -120,9 +137,8 @@ class GradBucketReducer:
         """Launch stragglers (unused params), wait for every bucket, reset counters."""
         if not self._sync:
             return
-        for bi in range(len(self.buckets)):
-            if self._handles[bi] is None:
-                self._launch(bi)
+        self._ready = [True] * len(self.buckets)
+        self._flush()
         for bi, h in enumerate(self._handles):
             h.wait()
             if self.average and not self._use_avg_op:
@@ -130,6 +146,8 @@ class GradBucketReducer:
                 self.arena.grads[b0:b1].div_(self.world)
         self._handles = [None] * len(self.buckets)
         self._arrived = [set() for _ in self.buckets]
+        self._ready = [False] * len(self.buckets)
+        self._cursor = 0
 
     def remove(self):
         for h in self._hooks:

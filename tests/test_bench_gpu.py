@@ -56,3 +56,14 @@ def test_bench_two_ranks_gloo_rehearsal():
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     _check(_json_line(out.stdout), 2, 2, 1, 4)
+
+
+def test_bench_self_spawns_two_ranks():
+    """No launcher: ``bench.py --gpus 2`` starts its own two ranks (gloo, sharing the one GPU
+    of the test box -- RCCL refuses two ranks on one device, and device_for says so)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "--micro-batch", "4", "--dist-backend", "gloo"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    _check(_json_line(out.stdout), 2, 2, 1, 4)

@@ -100,3 +100,65 @@ def test_tied_parameter_gets_its_own_bucket():
         red.remove()
     finally:
         dist.destroy_process_group()
+
+
+def test_collectives_launch_in_bucket_order():
+    """RCCL matches collectives by issue order: a bucket whose gradients land early must
+    wait until every bucket before it has launched (arrivals fed in reverse order)."""
+    from orion_amd.parallel.ddp import GradBucketReducer
+    from orion_amd.train.flat import FlatArena
+    port = _free_port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        model = build_gpt2("gpt2-tiny", block_size=32)
+        arena = FlatArena(model, dtype=torch.float32)
+        red = GradBucketReducer(arena, bucket_mb=0.05)
+        nb = len(red.buckets)
+        assert nb >= 4
+        red.launch_log = []
+        red.set_sync(True)
+        # every parameter of the LAST bucket first, then backwards through the buckets
+        for bi in reversed(range(nb)):
+            for s in red.buckets[bi][2]:
+                red._on_grad(s.param)
+            if bi > 0:
+                assert red.launch_log == [], "launched ahead of an unfinished earlier bucket"
+        assert red.launch_log == list(range(nb))
+        red.finish()
+        # an interleaved order: bucket 1 completes before bucket 0, then 0 releases both
+        red.launch_log = []
+        for s in red.buckets[1][2]:
+            red._on_grad(s.param)
+        assert red.launch_log == []
+        for s in red.buckets[0][2]:
+            red._on_grad(s.param)
+        assert red.launch_log == [0, 1]
+        red.finish()  # stragglers (buckets 2..) still go out in order
+        assert red.launch_log == list(range(nb))
+        red.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_spawns_its_own_ranks_on_cpu():
+    """``python bench.py --gpus 2`` with no launcher around it starts both ranks itself."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in
+           ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--model", "gpt2-tiny",
+                          "--device", "cpu", "--dist-backend", "gloo", "--seq-len", "64",
+                          "--micro-batch", "2", "--steps", "2", "--warmup", "1"],
+                         cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["steps"] == 2 and rec["warmup"] == 1
+    assert abs(rec["per_gpu"] * 2 - rec["value"]) / rec["value"] < 1e-3
+    assert rec["allreduce_busbw_gbps"] is not None

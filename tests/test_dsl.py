@@ -83,7 +83,8 @@ class TestSpaceBuilder:
         s = sb.build_from(["-x~uniform(-50, 50)", "--y~normal(0, 1)", "--plain", "5"])
         assert list(s.keys()) == ["/x", "/y"]
         t = Trial(params=[dict(name="/x", type="real", value=3.5), dict(name="/y", type="real", value=-1.0)])
-        assert sb.build_to(None, t) == ["--plain", "5", "-x=3.5", "--y=-1.0"]
+        # parameters render where they stood on the command line (the reference moved them last)
+        assert sb.build_to(None, t) == ["-x=3.5", "--y=-1.0", "--plain", "5"]
 
     def test_config_option(self, yaml_tmpl, tmp_path):
         sb = SpaceBuilder()
@@ -131,3 +132,21 @@ class TestSpaceBuilder:
         sb.build_from(["-x~uniform(0, 1)"])
         t = Trial(params=[dict(name="/x", type="real", value=np.float64(0.25))])
         assert sb.build_to(None, t) == ["-x=0.25"]
+
+
+def test_template_is_immutable_and_render_is_pure(tmp_path):
+    from orion_amd.space.dsl import Hole, ScriptTemplate
+    p = tmp_path / "c.yaml"
+    p.write_text(yaml.safe_dump({"opt": {"lr": "orion~loguniform(1e-4, 1e-1)"}, "keep": [1, 2]}))
+    tmpl = ScriptTemplate.parse(["pos0", "--config=" + str(p), "-x~uniform(0, 1)", "tail"])
+    assert tmpl.argv == ("pos0", Hole("/x", "-x"), "tail")
+    assert list(tmpl.space) == ["/x", "/opt/lr"]
+    with pytest.raises(Exception):
+        tmpl.argv = ()
+    t = Trial(params=[dict(name="/x", type="real", value=0.5), dict(name="/opt/lr", type="real", value=0.01)])
+    a = tmpl.render(t, str(tmp_path / "a.yaml"))
+    b = tmpl.render(t, str(tmp_path / "b.yaml"))
+    assert a[1:] == b[1:] == ["pos0", "-x=0.5", "tail"]
+    assert yaml.safe_load(open(tmp_path / "a.yaml")) == {"opt": {"lr": 0.01}, "keep": [1, 2]}
+    # the template document itself is untouched by rendering
+    assert tmpl.config_doc["opt"]["lr"].startswith("orion~")

@@ -153,6 +153,9 @@ def test_is_done_by_max_trials(storage):
         t.results = [Trial.Result(name="o", type="objective", value=1.0)]
         exp.push_completed_trial(t)
     assert exp.is_done
+    # the query has no side effect; finish_if_done records the status
+    assert storage.read("experiments", {"_id": exp.id})[0]["status"] == "pending"
+    assert exp.finish_if_done()
     assert storage.read("experiments", {"_id": exp.id})[0]["status"] == "done"
 
 
@@ -189,3 +192,32 @@ def test_fetch_tolerates_clock_skew(storage):
     exp.push_completed_trial(t)
     storage.write("trials", {"end_time": utcnow() - datetime.timedelta(minutes=2)}, {"_id": t.id})
     assert [x.id for x in exp.fetch_completed_trials()] == [t.id]
+
+
+def test_completion_is_a_cas_on_reserved(storage):
+    exp = _ready(storage)
+    Producer(exp).produce()
+    t = exp.reserve_trial(worker="w0")
+    # another worker's reaper re-queues the trial (stale heartbeat) and someone re-reserves it
+    storage.write("trials", {"status": "interrupted"}, {"_id": t.id})
+    t2 = exp.reserve_trial(worker="w1")
+    assert t2.id == t.id or exp.reserve_trial(worker="w1") is not None
+    t.results = [Trial.Result(name="o", type="objective", value=1.0)]
+    assert not exp.push_completed_trial(t, only_if_reserved=True)  # w0 lost it
+    doc = storage.read("trials", {"_id": t.id})[0]
+    assert doc["status"] in ("reserved", "interrupted") and doc.get("results", []) == []
+
+
+def test_plan_configuration_is_pure(storage):
+    from orion_amd.core.experiment import plan_configuration
+    exp = Experiment("p", storage, user="u")
+    cfg = _config(exp)
+    plan = plan_configuration(None, cfg)
+    assert plan.config["algorithms"] == {"random": {}} and list(plan.template.space) == ["/x"]
+    assert storage.count("experiments") == 0
+    same = dict(plan.config, max_trials=99)
+    assert plan_configuration(plan.config, same).config["max_trials"] == 99
+    other = copy_cfg = __import__("copy").deepcopy(plan.config)
+    copy_cfg["metadata"]["user_args"] = ["-x~uniform(0, 2)"]
+    with pytest.raises(NotImplementedError, match="metadata"):
+        plan_configuration(plan.config, other)
