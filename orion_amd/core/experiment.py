@@ -104,20 +104,37 @@ class Experiment:
         db.ensure_index("trials", [("end_time", db.DESCENDING)])
 
     # ------------------------------------------------------------------ trials
+    RESERVE_WINDOW = 64
+
+    def _candidates(self, query, uniform):
+        """Reservable trials to choose from.  When every candidate scores the same, a
+        random window of ``RESERVE_WINDOW`` of them is enough (one COUNT plus one paged read,
+        independent of how many trials are pending); otherwise all of them."""
+        if not uniform:
+            return Trial.build(self._db.read("trials", query))
+        n = self._db.count("trials", query)
+        if n == 0:
+            return []
+        skip = random.randrange(n - self.RESERVE_WINDOW + 1) if n > self.RESERVE_WINDOW else 0
+        return Trial.build(self._db.read("trials", query, skip=skip, limit=self.RESERVE_WINDOW))
+
     def reserve_trial(self, score_handle=None, worker=None):
-        """Atomically move one reservable trial to ``reserved``; None if there is none."""
+        """Atomically move one reservable trial to ``reserved``; None if there is none.
+        Among the candidates the best-scored ones win (``score_handle``), ties at random."""
         if score_handle is not None and not callable(score_handle):
             raise ValueError("Argument `score_handle` must be callable with a `Trial`.")
+        uniform = score_handle is None or bool(
+            getattr(getattr(score_handle, "__self__", None), "scores_uniform", False))
         for _ in range(self.MAX_RESERVE_ATTEMPTS):
             query = dict(experiment=self._id, status={"$in": list(Trial.reservable_stati)})
-            candidates = Trial.build(self._db.read("trials", query))
+            candidates = self._candidates(query, uniform)
             if not candidates:
                 return None
-            if score_handle is not None and self.space:
+            if score_handle is not None and not uniform and self.space:
                 scores = [score_handle(trial_to_tuple(t, self.space)) for t in candidates]
                 best = max(scores)
                 candidates = [t for s, t in zip(scores, candidates) if s == best]
-            elif score_handle is not None:
+            elif score_handle is not None and not uniform:
                 log.warning("`score_handle` given but the parameter space is not defined yet.")
             sel = random.sample(candidates, 1)[0]
             now = utcnow()

@@ -33,6 +33,13 @@ class PrimaryAlgo(BaseAlgorithm):
         assert point in self._space
         return self.algorithm.score(point)
 
+    @property
+    def scores_uniform(self):
+        """True when the algorithm keeps the default ``score`` (every point ties), so a
+        reservation may pick among a random window of candidates instead of scoring all."""
+        from ..algo.base import BaseAlgorithm
+        return type(self.algorithm).score is BaseAlgorithm.score
+
     def judge(self, point, measurements):
         assert point in self._space
         return self.algorithm.judge(point, measurements)

@@ -67,8 +67,8 @@ class AbstractDB(abc.ABC):
         None, else ``$set`` it on every matching document (upsert).  Returns #docs written."""
 
     @abc.abstractmethod
-    def read(self, collection_name, query=None, selection=None):
-        ...
+    def read(self, collection_name, query=None, selection=None, skip=0, limit=None):
+        """Matching documents in insertion order; ``skip``/``limit`` page through them."""
 
     @abc.abstractmethod
     def read_and_write(self, collection_name, query, data, selection=None):

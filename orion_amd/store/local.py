@@ -8,9 +8,17 @@ precondition) and unique-index checks are serialised exactly like MongoDB's
 single-document atomic ``find_one_and_update``.
 WAL journaling keeps readers unblocked while a writer holds the lock.
 
-Documents are stored as JSON (datetimes as ``{"$date": iso}``); the queried
-fields ``experiment`` and ``status`` are mirrored into indexed columns so a
-worker's poll does not parse every trial document.
+Documents are stored as JSON (datetimes as ``{"$date": iso}``).  Hot paths are
+indexed, so their cost does not grow with the number of trials:
+
+* ``_id`` is the primary key and ``experiment`` / ``status`` are mirrored into
+  indexed columns: a query that pins them by equality or ``$in`` is answered in
+  SQL (the reservation compare-and-swap ``{_id, status}`` touches one row);
+* ``count`` of such a query is ``SELECT COUNT(*)``; ``read(skip=, limit=)`` becomes
+  ``LIMIT/OFFSET``;
+* unique indexes are kept in a key table with a primary key on
+  ``(collection, fields, key)``, so an insert checks uniqueness with one index probe
+  instead of a scan of the collection.
 """
 from __future__ import annotations
 
@@ -28,6 +36,7 @@ from .base import AbstractDB, DatabaseError, DuplicateKeyError, normalize_index_
 from .query import apply_set, get_path, match, project
 
 _INDEXED = ("experiment", "status")
+_SQL_FIELDS = {"_id": "id", "experiment": "experiment", "status": "status"}
 
 
 def _default(o):
@@ -78,6 +87,9 @@ class LocalDB(AbstractDB):
             conn.execute("PRAGMA journal_mode=WAL")
             conn.execute("CREATE TABLE IF NOT EXISTS _orion_indexes "
                          "(coll TEXT, fields TEXT, uniq INTEGER, PRIMARY KEY (coll, fields))")
+            conn.execute("CREATE TABLE IF NOT EXISTS _orion_unique "
+                         "(coll TEXT, fields TEXT, key TEXT, id TEXT, PRIMARY KEY (coll, fields, key))")
+            conn.execute("CREATE INDEX IF NOT EXISTS _orion_unique_id ON _orion_unique (coll, id)")
         except sqlite3.Error as exc:
             raise DatabaseError(f"cannot open local database {self.path}: {exc}") from exc
         self._open = True
@@ -88,6 +100,9 @@ class LocalDB(AbstractDB):
             conn = sqlite3.connect(self.path, timeout=60.0, isolation_level=None,
                                    check_same_thread=False)
             conn.execute("PRAGMA busy_timeout=60000")
+            # WAL + NORMAL: commits are atomic and crash-safe; only an OS crash may lose the
+            # last transactions (no fsync per reservation)
+            conn.execute("PRAGMA synchronous=NORMAL")
             self._local.conn = conn
         return conn
 
@@ -130,40 +145,61 @@ class LocalDB(AbstractDB):
         rows = conn.execute("SELECT fields FROM _orion_indexes WHERE coll=? AND uniq=1", (coll,)).fetchall()
         return [tuple(json.loads(r[0])) for r in rows]
 
+    @staticmethod
+    def _sql_value(field, v):
+        return v if field == "_id" else json.dumps(v, default=_default)
+
     def _prefilter(self, query):
-        """SQL WHERE for the mirrored columns when the query pins them by equality / $in."""
-        where, args = [], []
-        for f in _INDEXED:
-            if not query or f not in query:
+        """SQL WHERE for ``_id`` and the mirrored columns where the query pins them by
+        equality / ``$in``; ``covered`` says whether SQL alone decides the match."""
+        where, args, covered = [], [], True
+        for f, cond in (query or {}).items():
+            col = _SQL_FIELDS.get(f)
+            if col is None:
+                covered = False
                 continue
-            cond = query[f]
-            if isinstance(cond, dict) and set(cond) == {"$in"}:
-                vals = [json.dumps(v, default=_default) for v in cond["$in"]]
-                where.append(f"{f} IN ({','.join('?' * len(vals))})")
+            if isinstance(cond, dict) and set(cond) == {"$in"} and \
+                    all(not isinstance(v, (dict, list)) for v in cond["$in"]):
+                vals = [self._sql_value(f, v) for v in cond["$in"]]
+                where.append(f"{col} IN ({','.join('?' * len(vals))})" if vals else "0")
                 args.extend(vals)
-            elif not isinstance(cond, (dict, list)):
-                where.append(f"{f} = ?")
-                args.append(json.dumps(cond, default=_default))
-        return (" WHERE " + " AND ".join(where)) if where else "", args
+            elif not isinstance(cond, (dict, list)) and cond is not None:
+                where.append(f"{col} = ?")
+                args.append(self._sql_value(f, cond))
+            else:
+                covered = False
+        return (" WHERE " + " AND ".join(where)) if where else "", args, covered
 
-    def _select(self, conn, coll, query):
+    def _select(self, conn, coll, query, skip=0, limit=None):
         self._table(conn, coll)
-        w, a = self._prefilter(query)
-        rows = conn.execute(f"SELECT doc FROM {self._q(coll)}{w}", a).fetchall()
+        w, a, covered = self._prefilter(query)
+        page = ""
+        if covered and (skip or limit is not None):
+            page = f" LIMIT {int(limit) if limit is not None else -1} OFFSET {int(skip)}"
+        rows = conn.execute(f"SELECT doc FROM {self._q(coll)}{w}{page}", a).fetchall()
         docs = (loads(r[0]) for r in rows)
-        return [d for d in docs if match(d, query)]
+        hits = [d for d in docs if match(d, query)]
+        if not page and (skip or limit is not None):
+            hits = hits[skip: None if limit is None else skip + limit]
+        return hits
 
-    def _check_unique(self, conn, coll, doc, exclude_id=None):
-        for fields in self._uniques(conn, coll):
-            key = tuple(get_path(doc, f) for f in fields)
-            for other in self._select(conn, coll, None):
-                if other["_id"] == exclude_id:
-                    continue
-                if tuple(get_path(other, f) for f in fields) == key:
-                    raise DuplicateKeyError(f"duplicate key {dict(zip(fields, map(repr, key)))} "
-                                            f"in {coll}")
+    def _unique_keys(self, conn, coll, doc):
+        return [(json.dumps(list(fields)), json.dumps([get_path(doc, f) for f in fields], default=_default))
+                for fields in self._uniques(conn, coll)]
+
+    def _claim_keys(self, conn, coll, doc, replace=False):
+        """Record ``doc``'s unique keys; DuplicateKeyError if another document holds one."""
+        if replace:
+            conn.execute("DELETE FROM _orion_unique WHERE coll=? AND id=?", (coll, doc["_id"]))
+        for fields, key in self._unique_keys(conn, coll, doc):
+            try:
+                conn.execute("INSERT INTO _orion_unique (coll, fields, key, id) VALUES (?,?,?,?)",
+                             (coll, fields, key, doc["_id"]))
+            except sqlite3.IntegrityError as exc:
+                raise DuplicateKeyError(f"duplicate key {fields}={key} in {coll}") from exc
 
     def _put(self, conn, coll, doc, insert):
+        self._claim_keys(conn, coll, doc, replace=not insert)
         vals = (doc["_id"], _col_value(doc, "experiment"), _col_value(doc, "status"), dumps(doc))
         if insert:
             try:
@@ -187,6 +223,22 @@ class LocalDB(AbstractDB):
             if unique:
                 conn.execute("UPDATE _orion_indexes SET uniq=1 WHERE coll=? AND fields=?",
                              (collection_name, fields))
+                # documents written before the index existed get their keys now
+                have = conn.execute("SELECT COUNT(*) FROM _orion_unique WHERE coll=? AND fields=?",
+                                    (collection_name, fields)).fetchone()[0]
+                total = conn.execute(f"SELECT COUNT(*) FROM {self._q(collection_name)}").fetchone()[0]
+                if have != total:
+                    conn.execute("DELETE FROM _orion_unique WHERE coll=? AND fields=?",
+                                 (collection_name, fields))
+                    flds = json.loads(fields)
+                    for d in self._select(conn, collection_name, None):
+                        key = json.dumps([get_path(d, f) for f in flds], default=_default)
+                        try:
+                            conn.execute("INSERT INTO _orion_unique (coll, fields, key, id) "
+                                         "VALUES (?,?,?,?)", (collection_name, fields, key, d["_id"]))
+                        except sqlite3.IntegrityError as exc:
+                            raise DuplicateKeyError(f"existing documents violate unique index "
+                                                    f"{fields} in {collection_name}") from exc
             conn.execute("COMMIT")
         except BaseException:
             conn.execute("ROLLBACK")
@@ -201,7 +253,6 @@ class LocalDB(AbstractDB):
                 docs = data if isinstance(data, list) else [data]
                 for d in docs:
                     d.setdefault("_id", uuid.uuid4().hex)
-                    self._check_unique(conn, collection_name, d)
                     self._put(conn, collection_name, d, insert=True)
                 n = len(docs)
             else:
@@ -210,13 +261,11 @@ class LocalDB(AbstractDB):
                     new = {k: v for k, v in query.items() if not isinstance(v, dict) and "." not in k}
                     apply_set(new, data)
                     new.setdefault("_id", uuid.uuid4().hex)
-                    self._check_unique(conn, collection_name, new)
                     self._put(conn, collection_name, new, insert=True)
                     n = 1
                 else:
                     for d in hits:
                         apply_set(d, data)
-                        self._check_unique(conn, collection_name, d, exclude_id=d["_id"])
                         self._put(conn, collection_name, d, insert=False)
                     n = len(hits)
             conn.execute("COMMIT")
@@ -225,20 +274,20 @@ class LocalDB(AbstractDB):
             conn.execute("ROLLBACK")
             raise
 
-    def read(self, collection_name, query=None, selection=None):
+    def read(self, collection_name, query=None, selection=None, skip=0, limit=None):
         conn = self._connect()
-        return [project(d, selection) for d in self._select(conn, collection_name, query)]
+        return [project(d, selection)
+                for d in self._select(conn, collection_name, query, skip, limit)]
 
     def read_and_write(self, collection_name, query, data, selection=None):
         conn = self._connect()
         self._begin(conn)
         try:
-            hits = self._select(conn, collection_name, query)
+            hits = self._select(conn, collection_name, query, limit=1)
             if not hits:
                 conn.execute("COMMIT")
                 return None
             d = apply_set(hits[0], data)
-            self._check_unique(conn, collection_name, d, exclude_id=d["_id"])
             self._put(conn, collection_name, d, insert=False)
             conn.execute("COMMIT")
             return project(d, selection)
@@ -248,6 +297,10 @@ class LocalDB(AbstractDB):
 
     def count(self, collection_name, query=None):
         conn = self._connect()
+        self._table(conn, collection_name)
+        w, a, covered = self._prefilter(query)
+        if covered:
+            return conn.execute(f"SELECT COUNT(*) FROM {self._q(collection_name)}{w}", a).fetchone()[0]
         return len(self._select(conn, collection_name, query))
 
     def remove(self, collection_name, query):
@@ -257,6 +310,7 @@ class LocalDB(AbstractDB):
             hits = self._select(conn, collection_name, query)
             for d in hits:
                 conn.execute(f"DELETE FROM {self._q(collection_name)} WHERE id=?", (d["_id"],))
+                conn.execute("DELETE FROM _orion_unique WHERE coll=? AND id=?", (collection_name, d["_id"]))
             conn.execute("COMMIT")
             return len(hits)
         except BaseException:

@@ -75,10 +75,11 @@ class MemoryDB(AbstractDB):
                 coll[d["_id"]] = cand
             return len(hits)
 
-    def read(self, collection_name, query=None, selection=None):
+    def read(self, collection_name, query=None, selection=None, skip=0, limit=None):
         with self._lock:
-            return [project(copy.deepcopy(d), selection)
-                    for d in self._coll(collection_name).values() if match(d, query)]
+            hits = [d for d in self._coll(collection_name).values() if match(d, query)]
+            hits = hits[skip: None if limit is None else skip + limit]
+            return [project(copy.deepcopy(d), selection) for d in hits]
 
     def read_and_write(self, collection_name, query, data, selection=None):
         with self._lock:

@@ -46,34 +46,44 @@ def mongodb_exception_wrapper(method):
 
 
 class MongoDB(AbstractDB):
-    """``host`` may be a hostname or a full ``mongodb://`` URI."""
+    """``host`` may be a hostname or a full ``mongodb://user:pw@host:port/db`` URI; fields
+    given explicitly (``port=``, ``name=``, ``username=``, ``password=``) override the
+    URI's (reference ``mongodb.py:237-255``).  ``check_connection=False`` skips the
+    initial round trip (pymongo connects lazily), e.g. to inspect a configuration."""
+
+    DEFAULT_PORT = 27017
 
     @mongodb_exception_wrapper
     def initiate_connection(self):
         if pymongo is None:
             raise DatabaseError("pymongo is not installed")
+        check = self.options.pop("check_connection", True)
         self._sanitize_attrs()
-        kw = dict(self.options)
+        kw = dict(self._uri_options)
+        kw.update(self.options)
         kw.setdefault("serverSelectionTimeoutMS", 5000)
         if self.username:
             kw.update(username=self.username, password=self.password, authSource=self.name)
         self._conn = pymongo.MongoClient(host=self.host, port=self.port, **kw)
         self._db = self._conn[self.name]
-        self._conn.admin.command("ping")
+        if check:
+            self._conn.admin.command("ping")
 
     def _sanitize_attrs(self):
-        if self.host and str(self.host).startswith("mongodb://"):
+        self._uri_options = {}
+        if self.host and str(self.host).startswith(("mongodb://", "mongodb+srv://")):
             from pymongo.uri_parser import parse_uri
-            info = parse_uri(self.host)
+            info = parse_uri(self.host, validate=False)
+            nodes = info.get("nodelist") or [("localhost", self.DEFAULT_PORT)]
+            self.host = nodes[0][0]
+            self.port = self.port if self.port is not None else nodes[0][1]
             self.username = self.username or info.get("username")
             self.password = self.password or info.get("password")
             self.name = self.name or info.get("database")
-            nodes = info.get("nodelist") or []
-            if nodes and self.port is None:
-                self.port = nodes[0][1]
+            self._uri_options = dict(info.get("options") or {})
+        self.host = self.host or "localhost"
+        self.port = int(self.port) if self.port is not None else self.DEFAULT_PORT
         self.name = self.name or "orion"
-        if self.port is not None:
-            self.port = int(self.port)
 
     @property
     def is_connected(self):
@@ -105,8 +115,13 @@ class MongoDB(AbstractDB):
         return res.modified_count or (1 if res.upserted_id is not None else 0)
 
     @mongodb_exception_wrapper
-    def read(self, collection_name, query=None, selection=None):
-        return list(self._db[collection_name].find(query or {}, selection))
+    def read(self, collection_name, query=None, selection=None, skip=0, limit=None):
+        cur = self._db[collection_name].find(query or {}, selection)
+        if skip:
+            cur = cur.skip(int(skip))
+        if limit is not None:
+            cur = cur.limit(int(limit))
+        return list(cur)
 
     @mongodb_exception_wrapper
     def read_and_write(self, collection_name, query, data, selection=None):
