@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: plumbing rehearsal (reference ops, gloo) -- not a measurement")
     ap.add_argument("--no-busbw", action="store_true", help="skip the post-run all-reduce probe")
+    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="gradient arena dtype (fp32: accumulation and all-reduce in fp32)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the whole training step in a HIP graph (single GPU)")
     return ap.parse_args()
@@ -121,7 +123,8 @@ def main():
 
     ocfg = OptimConfig(warmup_iters=10, lr_decay_iters=10000)
     if args.impl == "native":
-        trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb, graph=args.hip_graph and world == 1)
+        trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb, graph=args.hip_graph and world == 1,
+                          grad_dtype=torch.float32 if args.grad_dtype == "fp32" else torch.bfloat16)
         step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
     else:
         ddp_model = model

@@ -124,27 +124,35 @@ __global__ __launch_bounds__(256) void scale_bf16_kernel(bf16_t* __restrict__ x,
   }
 }
 
-// out[i] = bf16( (*scale) * sum_s slabs[s][i] ): the combine step of the split-K weight
-// gradient (S fp32 slabs from one batched GEMM over token chunks), with the LM head's
-// 1/n_valid * upstream-grad scale folded in.  Fixed summation order: deterministic.
+// out[i] = (*scale) * sum_s slabs[s][i] (+ out[i] when accumulating): the combine step of
+// the split-K weight gradient (S fp32 slabs from one launch over token chunks), with the
+// LM head's 1/n_valid * upstream-grad scale folded in.  out is the parameter's slice of
+// the gradient arena, fp32 (f32 != 0) or bf16.  Fixed summation order: deterministic.
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slabs, int S,
-                                                       long n4, bf16_t* __restrict__ out,
+                                                       long n4, void* __restrict__ out,
                                                        const float* __restrict__ scale,
-                                                       int accumulate) {
+                                                       int accumulate, int f32) {
   const float sc = scale ? *scale : 1.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     f32x4 acc = reinterpret_cast<const f32x4*>(slabs)[i];
     for (int k = 1; k < S; ++k) acc += reinterpret_cast<const f32x4*>(slabs + (long)k * n4 * 4)[i];
-    bf16x4 o;
-    if (accumulate) {  // += into the gradient arena (micro-batch accumulation, tied weights)
-      const bf16x4 prev = reinterpret_cast<const bf16x4*>(out)[i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = f2bf(fmaf(acc[j], sc, bf2f(prev[j])));
+    acc *= sc;
+    if (f32) {
+      f32x4* o = reinterpret_cast<f32x4*>(out) + i;
+      *o = accumulate ? *o + acc : acc;
     } else {
+      bf16x4* o = reinterpret_cast<bf16x4*>(out) + i;
+      bf16x4 r;
+      if (accumulate) {
+        const bf16x4 prev = *o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[j] * sc);
+        for (int j = 0; j < 4; ++j) r[j] = f2bf(acc[j] + bf2f(prev[j]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = f2bf(acc[j]);
+      }
+      *o = r;
     }
-    reinterpret_cast<bf16x4*>(out)[i] = o;
   }
 }
 
@@ -201,9 +209,9 @@ int orion_scale_bf16(void* x, const float* scale, long n, hipStream_t st) {
 }
 
 int orion_slab_sum(const float* slabs, int S, long n, void* out, const float* scale,
-                   int accumulate, hipStream_t st) {
+                   int accumulate, int out_f32, hipStream_t st) {
   if (n % 4) return -1;
   const long n4 = n / 4;
-  slab_sum_kernel<<<ew_grid(n4 / 2), 256, 0, st>>>(slabs, S, n4, (bf16_t*)out, scale, accumulate);
+  slab_sum_kernel<<<ew_grid(n4 / 2), 256, 0, st>>>(slabs, S, n4, out, scale, accumulate, out_f32);
   return (int)hipGetLastError();
 }

@@ -1,6 +1,6 @@
 // Fused AdamW over the flat parameter arena (K8 in SURVEY.md §2.11).
 //
-// One pass over numel elements: reads bf16 grad, fp32 master/exp_avg/exp_avg_sq
+// One pass over numel elements: reads the fp32 (default) or bf16 grad, fp32 master/exp_avg/exp_avg_sq
 // and a per-2048-element-chunk weight-decay flag; writes master/m/v and the bf16
 // compute copy.  Hyper-parameters (lr, betas, eps, wd, bias corrections, clip)
 // and the global gradient sum-of-squares are read from DEVICE memory, so a
@@ -12,18 +12,39 @@ namespace orion {
 
 constexpr int ADAM_CHUNK = 2048;  // must match orion_amd/train/flat.py ALIGN
 
+// 8 consecutive gradient elements as fp32 (arena in fp32 or bf16)
+ORION_DEVICE void load8(const float* g, long e, float (&f)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(g + e), b = *reinterpret_cast<const f32x4*>(g + e + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { f[j] = a[j]; f[4 + j] = b[j]; }
+}
+ORION_DEVICE void load8(const bf16_t* g, long e, float (&f)[8]) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + e);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
+}
+ORION_DEVICE void load4(const float* g, long e, float (&f)[4]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(g + e);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f[j] = a[j];
+}
+ORION_DEVICE void load4(const bf16_t* g, long e, float (&f)[4]) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(g + e);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f[j] = bf2f(v[j]);
+}
+
 // partial[b] = sum of squares over this workgroup's grid-stride slice
-__global__ __launch_bounds__(256) void sumsq_partial_kernel(const bf16_t* __restrict__ g, long n8,
+template <typename G>
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const G* __restrict__ g, long n8,
                                                             float* __restrict__ partial) {
   __shared__ float red[4];
   float s = 0.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(g + i * 8);
+    float v[8];
+    load8(g, i * 8, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = bf2f(v[j]);
-      s += f * f;
-    }
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
   }
   s = block_sum<4>(s, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = s;
@@ -39,9 +60,10 @@ __global__ __launch_bounds__(1024) void sum_partials_kernel(const float* __restr
 }
 
 // hyper = [lr, beta1, beta2, eps, weight_decay, 1-beta1^t, 1-beta2^t, max_grad_norm]
+template <typename G>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(
     bf16_t* __restrict__ p16, float* __restrict__ master, float* __restrict__ m,
-    float* __restrict__ v, const bf16_t* __restrict__ g, const uint8_t* __restrict__ decay,
+    float* __restrict__ v, const G* __restrict__ g, const uint8_t* __restrict__ decay,
     const float* __restrict__ hyper, const float* __restrict__ sumsq, long n4) {
   const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float bc1 = hyper[5], bc2 = hyper[6], clip = hyper[7];
@@ -58,11 +80,12 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
     f32x4 w = *reinterpret_cast<const f32x4*>(master + e);
     f32x4 mm = *reinterpret_cast<const f32x4*>(m + e);
     f32x4 vv = *reinterpret_cast<const f32x4*>(v + e);
-    bf16x4 gg = *reinterpret_cast<const bf16x4*>(g + e);
+    float gg[4];
+    load4(g, e, gg);
     bf16x4 out;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float gr = bf2f(gg[j]) * cs;
+      const float gr = gg[j] * cs;
       mm[j] = b1 * mm[j] + (1.f - b1) * gr;
       vv[j] = b2 * vv[j] + (1.f - b2) * gr * gr;
       const float denom = sqrtf(vv[j] * inv_bc2) + eps;
@@ -84,22 +107,27 @@ constexpr int SUMSQ_BLOCKS = 1024;
 
 int orion_sumsq_partials() { return SUMSQ_BLOCKS; }
 
-// out[0] = sum(g^2); partial holds SUMSQ_BLOCKS floats.
-int orion_grad_sumsq(const void* g, long n, float* partial, float* out, hipStream_t st) {
+// out[0] = sum(g^2) over an fp32 (g_f32) or bf16 arena; partial holds SUMSQ_BLOCKS floats.
+int orion_grad_sumsq(const void* g, long n, int g_f32, float* partial, float* out, hipStream_t st) {
   if (n % 8) return -1;
-  sumsq_partial_kernel<<<SUMSQ_BLOCKS, 256, 0, st>>>((const bf16_t*)g, n / 8, partial);
+  if (g_f32) sumsq_partial_kernel<float><<<SUMSQ_BLOCKS, 256, 0, st>>>((const float*)g, n / 8, partial);
+  else sumsq_partial_kernel<bf16_t><<<SUMSQ_BLOCKS, 256, 0, st>>>((const bf16_t*)g, n / 8, partial);
   sum_partials_kernel<<<1, 1024, 0, st>>>(partial, SUMSQ_BLOCKS, out);
   return (int)hipGetLastError();
 }
 
-int orion_adamw_flat(void* p16, float* master, float* m, float* v, const void* g,
+int orion_adamw_flat(void* p16, float* master, float* m, float* v, const void* g, int g_f32,
                      const uint8_t* decay, const float* hyper, const float* sumsq, long n,
                      hipStream_t st) {
   if (n % ADAM_CHUNK) return -1;
   const long n4 = n / 4;
   long grid = (n4 + 255) / 256;
   if (grid > 4096) grid = 4096;
-  adamw_flat_kernel<<<(int)grid, 256, 0, st>>>((bf16_t*)p16, master, m, v, (const bf16_t*)g,
-                                               decay, hyper, sumsq, n4);
+  if (g_f32)
+    adamw_flat_kernel<float><<<(int)grid, 256, 0, st>>>((bf16_t*)p16, master, m, v, (const float*)g,
+                                                        decay, hyper, sumsq, n4);
+  else
+    adamw_flat_kernel<bf16_t><<<(int)grid, 256, 0, st>>>((bf16_t*)p16, master, m, v,
+                                                         (const bf16_t*)g, decay, hyper, sumsq, n4);
   return (int)hipGetLastError();
 }

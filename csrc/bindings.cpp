@@ -20,30 +20,30 @@ int orion_layernorm_fwd(const void*, const void*, const void*, void*, float*, fl
                         float, const void*, void*, const void*, hipStream_t);
 int orion_layernorm_bwd_blocks(int rows);
 int orion_layernorm_bwd(const void*, const void*, const void*, const float*, const float*, void*,
-                        void*, void*, float*, int, int, const void*, void*, hipStream_t);
-int orion_colsum_bf16(const void*, void*, float*, int, int, hipStream_t);
+                        void*, void*, float*, int, int, const void*, void*, int, hipStream_t);
+int orion_colsum_bf16(const void*, void*, float*, int, int, int, hipStream_t);
 int orion_bias_gelu_fwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_bias_gelu_bwd(const void*, const void*, const void*, void*, float*, int, int, hipStream_t);
-int orion_colsum_partials2(const float*, float*, void*, int, int, hipStream_t);
+int orion_colsum_partials2(const float*, float*, void*, int, int, int, hipStream_t);
 int orion_colsum_scratch(int rows, int C);
 int orion_swiglu_fwd(const void*, void*, long, int, hipStream_t);
 int orion_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
 int orion_scale_bf16(void*, const float*, long, hipStream_t);
-int orion_slab_sum(const float*, int, long, void*, const float*, int, hipStream_t);
+int orion_slab_sum(const float*, int, long, void*, const float*, int, int, hipStream_t);
 int orion_wgrad_splits(int, int, int);
 int orion_wgrad_effective_splits(int, int);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
-                const float*, int, hipStream_t);
+                const float*, int, int, hipStream_t);
 int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
 int orion_sumsq_partials();
-int orion_grad_sumsq(const void*, long, float*, float*, hipStream_t);
-int orion_adamw_flat(void*, float*, float*, float*, const void*, const uint8_t*, const float*,
+int orion_grad_sumsq(const void*, long, int, float*, float*, hipStream_t);
+int orion_adamw_flat(void*, float*, float*, float*, const void*, int, const uint8_t*, const float*,
                      const float*, long, hipStream_t);
 int orion_rmsnorm_fwd(const void*, const void*, void*, float*, int, int, float, const void*, void*,
                       hipStream_t);
 int orion_rmsnorm_bwd_blocks(int rows);
 int orion_rmsnorm_bwd(const void*, const void*, const void*, const float*, void*, void*, float*,
-                      int, int, const void*, hipStream_t);
+                      int, int, const void*, int, hipStream_t);
 int orion_rope(const void*, long, long, long, void*, long, long, long, const float*, const float*,
                int, int, int, int, int, float, hipStream_t);
 int orion_attn_fwd(const orion::AttnParams&, int, bool, hipStream_t);
@@ -67,10 +67,20 @@ void check_bf16(const Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
 }
 
-// an optional in-place output: must be a contiguous bf16 vector of n elements
+// a gradient output: bf16, or fp32 (the gradient arena's default dtype)
+void check_grad_out(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name,
+              " must be bfloat16 or float32, got ", t.scalar_type());
+}
+
+int is_f32(const Tensor& t) { return t.scalar_type() == at::kFloat ? 1 : 0; }
+
+// an optional in-place output (a parameter's gradient-arena slice, ops/grad_sink.py): must be
+// a contiguous bf16 or fp32 vector of n elements
 bool has_out(const c10::optional<Tensor>& o, int64_t n, const char* name) {
   if (!o.has_value() || !o->defined()) return false;
-  check_bf16(*o, name);
+  check_grad_out(*o, name);
   TORCH_CHECK(o->is_contiguous() && o->numel() == n, name, " must be contiguous with ", n,
               " elements, got ", o->sizes());
   return true;
@@ -155,11 +165,20 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const
   // and its return slot is left undefined
   const bool w_in = has_out(dw_out, C, "dw_out"), b_in = has_bias && has_out(db_out, C, "db_out");
   const bool s_in = want_dx_colsum && has_out(dxs_out, C, "dxs_out");
-  Tensor dw = w_in ? *dw_out : at::empty({C}, w.options());
-  Tensor db = has_bias ? (b_in ? *db_out : at::empty({C}, w.options())) : Tensor();
+  // one output dtype for the three column sums: fp32 if any given slice is fp32 (the caller
+  // converts returned gradients to the parameter dtype)
+  int f32 = 0;
+  for (auto* o : {&dw_out, &db_out, &dxs_out})
+    if (o->has_value() && (*o)->defined()) f32 |= is_f32(**o);
+  for (auto* o : {&dw_out, &db_out, &dxs_out})
+    if (o->has_value() && (*o)->defined())
+      TORCH_CHECK(is_f32(**o) == f32, "layernorm_bwd: gradient outputs must share one dtype");
+  auto gopts = f32 ? w.options().dtype(at::kFloat) : w.options();
+  Tensor dw = w_in ? *dw_out : at::empty({C}, gopts);
+  Tensor db = has_bias ? (b_in ? *db_out : at::empty({C}, gopts)) : Tensor();
   const int nb = orion_layernorm_bwd_blocks(rows);
   auto part = at::empty({3 * (long)nb * C + 48L * C}, x.options().dtype(at::kFloat));
-  Tensor dxs = want_dx_colsum ? (s_in ? *dxs_out : at::empty({C}, x.options())) : Tensor();
+  Tensor dxs = want_dx_colsum ? (s_in ? *dxs_out : at::empty({C}, f32 ? gopts : x.options())) : Tensor();
   Tensor drc;
   if (dres.has_value() && dres->defined()) {
     check_bf16(*dres, "dres");
@@ -169,7 +188,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
                                    dw.data_ptr(), has_bias ? db.data_ptr() : nullptr,
                                    part.data_ptr<float>(), rows, C, drc.defined() ? drc.data_ptr() : nullptr,
-                                   want_dx_colsum ? dxs.data_ptr() : nullptr, cur_stream()),
+                                   want_dx_colsum ? dxs.data_ptr() : nullptr, f32, cur_stream()),
                "layernorm_bwd");
   return {dx, w_in ? Tensor() : dw, b_in ? Tensor() : db, s_in ? Tensor() : dxs};
 }
@@ -218,7 +237,7 @@ std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& x,
   if (part) {
     const int nb = orion_layernorm_bwd_blocks(rows);
     check_launch(orion_colsum_partials2(part, part + (long)nb * C, db.data_ptr(), nb, C,
-                                        cur_stream()),
+                                        is_f32(db), cur_stream()),
                  "colsum");
   }
   return {dx, (db.defined() && has_out(db_out, C, "db_out")) ? Tensor() : db};
@@ -234,7 +253,7 @@ Tensor colsum(const Tensor& m, const c10::optional<Tensor>& out_) {
   auto out = given ? *out_ : at::empty({C}, m.options());
   auto part = at::empty({(long)orion_colsum_scratch(rows, C)}, m.options().dtype(at::kFloat));
   check_launch(orion_colsum_bf16(mc.data_ptr(), out.data_ptr(), part.data_ptr<float>(), rows, C,
-                                 cur_stream()),
+                                 is_f32(out), cur_stream()),
                "colsum");
   return out;
 }
@@ -304,20 +323,20 @@ Tensor slab_sum(const Tensor& slabs, const c10::optional<Tensor>& scale) {
     TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "scale must be one fp32");
     sc = scale->data_ptr<float>();
   }
-  check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc, 0,
+  check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc, 0, 0,
                               cur_stream()),
                "slab_sum");
   return out;
 }
 
-// dW = dy^T x over the token dim (csrc/wgrad.hip) into out (N1, N2) contiguous bf16:
-// overwritten, or added to when accumulate (the gradient arena across micro-batches / tied
-// weights).  splits = 0 picks the split-K count.
+// dW = dy^T x over the token dim (csrc/wgrad.hip) into out (N1, N2) contiguous fp32 (the
+// gradient arena) or bf16: overwritten, or added to when accumulate (micro-batch
+// accumulation / tied weights).  splits = 0 picks the split-K count.
 void wgrad_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& scale, Tensor out,
                 bool accumulate, int64_t splits) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
-  check_bf16(out, "out");
+  check_grad_out(out, "out");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad: dy (M,N1), x (M,N2)");
   TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad: rows must be contiguous");
   const int M = dy.size(0), N1 = dy.size(1), N2 = x.size(1);
@@ -332,12 +351,13 @@ void wgrad_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& 
   if (S > 1) {
     auto slabs = at::empty({S, N1, N2}, dy.options().dtype(at::kFloat));
     check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, S,
-                             slabs.data_ptr<float>(), nullptr, nullptr, 0, cur_stream()), "wgrad");
+                             slabs.data_ptr<float>(), nullptr, nullptr, 0, 0, cur_stream()), "wgrad");
     check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc,
-                                accumulate ? 1 : 0, cur_stream()), "wgrad slab_sum");
+                                accumulate ? 1 : 0, is_f32(out), cur_stream()), "wgrad slab_sum");
   } else {
     check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, 1,
-                             nullptr, out.data_ptr(), sc, accumulate ? 1 : 0, cur_stream()), "wgrad");
+                             nullptr, out.data_ptr(), sc, accumulate ? 1 : 0, is_f32(out),
+                             cur_stream()), "wgrad");
   }
 }
 
@@ -351,10 +371,10 @@ int64_t wgrad_splits(int64_t M, int64_t N1, int64_t N2) { return orion_wgrad_spl
 
 // ------------------------------------------------------------------ optimizer
 void grad_sumsq(const Tensor& g, Tensor out) {
-  check_bf16(g, "grads");
+  check_grad_out(g, "grads");
   c10::hip::HIPGuardMasqueradingAsCUDA gd(g.device());
   auto part = at::empty({orion_sumsq_partials()}, g.options().dtype(at::kFloat));
-  check_launch(orion_grad_sumsq(g.data_ptr(), g.numel(), part.data_ptr<float>(),
+  check_launch(orion_grad_sumsq(g.data_ptr(), g.numel(), is_f32(g), part.data_ptr<float>(),
                                 out.data_ptr<float>(), cur_stream()),
                "grad_sumsq");
 }
@@ -362,7 +382,7 @@ void grad_sumsq(const Tensor& g, Tensor out) {
 void adamw_flat(Tensor p16, Tensor master, Tensor m, Tensor v, const Tensor& grad,
                 const Tensor& decay, const Tensor& hyper, const Tensor& sumsq) {
   check_bf16(p16, "params");
-  check_bf16(grad, "grads");
+  check_grad_out(grad, "grads");
   TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
                   v.scalar_type() == at::kFloat, "optimizer state must be fp32");
   TORCH_CHECK(decay.scalar_type() == at::kByte, "decay flags must be uint8");
@@ -371,7 +391,8 @@ void adamw_flat(Tensor p16, Tensor master, Tensor m, Tensor v, const Tensor& gra
               "arena size mismatch");
   c10::hip::HIPGuardMasqueradingAsCUDA g(p16.device());
   check_launch(orion_adamw_flat(p16.data_ptr(), master.data_ptr<float>(), m.data_ptr<float>(),
-                                v.data_ptr<float>(), grad.data_ptr(), decay.data_ptr<uint8_t>(),
+                                v.data_ptr<float>(), grad.data_ptr(), is_f32(grad),
+                                decay.data_ptr<uint8_t>(),
                                 hyper.data_ptr<float>(), sumsq.data_ptr<float>(), n, cur_stream()),
                "adamw_flat");
 }
@@ -430,7 +451,7 @@ std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const 
   check_launch(orion_rmsnorm_bwd(dyc.data_ptr(), xc.data_ptr(), w.contiguous().data_ptr(),
                                  rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr(),
                                  part.data_ptr<float>(), rows, C,
-                                 drc.defined() ? drc.data_ptr() : nullptr, cur_stream()),
+                                 drc.defined() ? drc.data_ptr() : nullptr, 0, cur_stream()),
                "rmsnorm_bwd");
   return {dx, dw};
 }

@@ -40,6 +40,18 @@ ORION_DEVICE unsigned pack_bf16x2(float lo, float hi) {
   return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
 }
 
+// Gradient-arena element I/O: the arena is fp32 by default (accumulation over micro-batches
+// and the data-parallel reduction stay in fp32) or bf16 (opt-in); kernels that write a
+// parameter's gradient slice take `void*` + a wave-uniform `f32` flag.
+ORION_DEVICE void store_grad(void* p, long i, float v, int f32) {
+  if (f32) static_cast<float*>(p)[i] = v;
+  else static_cast<bf16_t*>(p)[i] = f2bf(v);
+}
+
+ORION_DEVICE float load_grad(const void* p, long i, int f32) {
+  return f32 ? static_cast<const float*>(p)[i] : bf2f(static_cast<const bf16_t*>(p)[i]);
+}
+
 template <int N>
 struct VecT;
 template <>

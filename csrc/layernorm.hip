@@ -266,12 +266,13 @@ __global__ __launch_bounds__(256) void colsum_stage1_kernel(const float* __restr
 }
 
 __global__ __launch_bounds__(256) void colsum_stage2_kernel(const float* __restrict__ mid,
-                                                            bf16_t* __restrict__ out, int S, int C) {
+                                                            void* __restrict__ out, int S, int C,
+                                                            int f32) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   float s = 0.f;
   for (int i = 0; i < S; ++i) s += mid[(size_t)i * C + c];
-  out[c] = f2bf(s);
+  store_grad(out, c, s, f32);
 }
 
 constexpr int COLSUM_SPLITS = 16;
@@ -280,7 +281,8 @@ constexpr int COLSUM_SPLITS = 16;
 // pair: blockIdx.z picks the [P][C] partial matrix part + z*P*C; z whose output is
 // null is skipped (block-uniform exit, before any barrier).
 struct ColsumOuts {
-  bf16_t* out[3];
+  void* out[3];
+  int f32;  // outputs are fp32 (gradient arena) rather than bf16
 };
 
 __global__ __launch_bounds__(256) void colsum3_stage1_kernel(const float* __restrict__ part,
@@ -313,20 +315,21 @@ __global__ __launch_bounds__(256) void colsum3_stage1_kernel(const float* __rest
 
 __global__ __launch_bounds__(256) void colsum3_stage2_kernel(const float* __restrict__ mid, int S,
                                                              int C, ColsumOuts o) {
-  bf16_t* out = o.out[blockIdx.y];
+  void* out = o.out[blockIdx.y];
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (!out || c >= C) return;
   const float* mz = mid + (size_t)blockIdx.y * S * C;
   float s = 0.f;
   for (int i = 0; i < S; ++i) s += mz[(size_t)i * C + c];
-  out[c] = f2bf(s);
+  store_grad(out, c, s, o.f32);
 }
 
 }  // namespace orion
 
 using namespace orion;
 
-int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, hipStream_t st);
+int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, int f32,
+                           hipStream_t st);
 
 // exact_fit: 4-wide slices when they tile the row exactly and 8-wide ones would not
 // (C = 768: 3 x 64 x 4 uses every lane, 2 x 64 x 8 leaves a third idle).  Measured on
@@ -385,7 +388,7 @@ int orion_layernorm_bwd_blocks(int rows) {
 
 int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
                         const float* rstd, void* dx, void* dw, void* db, float* part, int rows,
-                        int C, const void* dres, void* drbias, hipStream_t st) {
+                        int C, const void* dres, void* drbias, int grad_f32, hipStream_t st) {
   int vec, it;
   if (!ln_pick(C, &vec, &it, /*exact_fit=*/true)) return -1;
   const int nb = orion_layernorm_bwd_blocks(rows);
@@ -414,7 +417,7 @@ int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const floa
   }
   float* mid = part + 3 * (size_t)nb * C;
   if (dw || db || drbias) {
-    const ColsumOuts o{{(bf16_t*)dw, (bf16_t*)db, (bf16_t*)drbias}};
+    const ColsumOuts o{{dw, db, drbias}, grad_f32};
     const int rps = (nb + COLSUM_SPLITS - 1) / COLSUM_SPLITS;
     colsum3_stage1_kernel<<<dim3((C + 63) / 64, COLSUM_SPLITS, 3), 256, 0, st>>>(part, mid, nb, C, rps, o);
     colsum3_stage2_kernel<<<dim3((C + 255) / 256, 3), 256, 0, st>>>(mid, COLSUM_SPLITS, C, o);
@@ -450,22 +453,24 @@ __global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(
   }
 }
 
-int orion_colsum_bf16(const void* m, void* out, float* part, int rows, int C, hipStream_t st) {
+int orion_colsum_bf16(const void* m, void* out, float* part, int rows, int C, int out_f32,
+                      hipStream_t st) {
   if (C % 8) return -1;
   const int nb = orion_layernorm_bwd_blocks(rows);
   const int rpb = (rows + nb - 1) / nb;
   dim3 grid(nb, (C / 8 + 63) / 64);
   colsum_bf16_partial_kernel<<<grid, 256, 0, st>>>((const bf16_t*)m, part, rows, C, rpb);
-  orion_colsum_partials2(part, part + (size_t)nb * C, out, nb, C, st);
+  orion_colsum_partials2(part, part + (size_t)nb * C, out, nb, C, out_f32, st);
   return (int)hipGetLastError();
 }
 
-// part[P][C] partials; mid: COLSUM_SPLITS * C floats of scratch
-int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, hipStream_t st) {
+// part[P][C] partials; mid: COLSUM_SPLITS * C floats of scratch; out fp32 when f32
+int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, int f32,
+                           hipStream_t st) {
   const int S = P < COLSUM_SPLITS ? (P < 1 ? 1 : P) : COLSUM_SPLITS;
   const int rps = (P + S - 1) / S;
   colsum_stage1_kernel<<<dim3((C + 63) / 64, S), 256, 0, st>>>(part, mid, P, C, rps);
-  colsum_stage2_kernel<<<(C + 255) / 256, 256, 0, st>>>(mid, (bf16_t*)out, S, C);
+  colsum_stage2_kernel<<<(C + 255) / 256, 256, 0, st>>>(mid, out, S, C, f32);
   return (int)hipGetLastError();
 }
 

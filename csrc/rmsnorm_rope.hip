@@ -181,7 +181,8 @@ __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* x, long xsb, lo
 
 using namespace orion;
 
-int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, hipStream_t st);
+int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, int f32,
+                           hipStream_t st);
 
 static int rms_blocks(int rows) { return rows < 1024 ? rows : 1024; }
 
@@ -204,7 +205,8 @@ int orion_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int ro
 int orion_rmsnorm_bwd_blocks(int rows) { return rms_blocks(rows); }
 
 int orion_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                      void* dw, float* part, int rows, int C, const void* dres, hipStream_t st) {
+                      void* dw, float* part, int rows, int C, const void* dres, int dw_f32,
+                      hipStream_t st) {
   if (C % 8) return -1;
   const int it = (C / 8 + 255) / 256;
   const int nb = rms_blocks(rows);
@@ -217,7 +219,7 @@ int orion_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float*
 #undef RB
     default: return -2;
   }
-  if (dw) return orion_colsum_partials2(part, part + (size_t)nb * C, dw, nb, C, st);
+  if (dw) return orion_colsum_partials2(part, part + (size_t)nb * C, dw, nb, C, dw_f32, st);
   return (int)hipGetLastError();
 }
 

@@ -83,7 +83,7 @@ template <int KS, int NS, int WM>
 __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
     const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B, long ldb, int M, int N1,
     int N2, int tiles_n2, int ntiles, int chunk, float* __restrict__ slabs,
-    bf16_t* __restrict__ out, const float* __restrict__ scale, int accumulate) {
+    void* __restrict__ out, const float* __restrict__ scale, int accumulate, int out_f32) {
   constexpr int BK = 16 * KS;        // m rows per stage
   constexpr int IMG = BK * 128;      // one [BK][128] image
   constexpr int STAGE = 4 * IMG;     // A halves 0,1 | B halves 0,1
@@ -207,8 +207,8 @@ __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
           else {
             const long o = (long)n1 * N2 + n2;
             float v = acc[a][b][r] * sc;
-            if (accumulate) v += bf2f(out[o]);  // gradient accumulation into the arena
-            out[o] = f2bf(v);
+            if (accumulate) v += load_grad(out, o, out_f32);  // accumulation into the arena
+            store_grad(out, o, v, out_f32);
           }
         }
       }
@@ -277,10 +277,11 @@ int orion_wgrad_lds() {
 }
 
 // A (M x N1, ld lda), B (M x N2, ld ldb) bf16 -> slabs (S, N1, N2) fp32 when S > 1
-// (caller folds them), else out (N1, N2) bf16 scaled by *scale (nullable), added to the
-// bf16 values already in out when accumulate != 0.
+// (caller folds them), else out (N1, N2; fp32 when out_f32, else bf16) scaled by *scale
+// (nullable), added to the values already in out when accumulate != 0.
 int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1, int N2, int S,
-                float* slabs, void* out, const float* scale, int accumulate, hipStream_t st) {
+                float* slabs, void* out, const float* scale, int accumulate, int out_f32,
+                hipStream_t st) {
   const int BK = wg_bk();
   if (M % BK || N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || N1 < 8 || N2 < 8) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -2;
@@ -294,7 +295,6 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   auto Ab = (const bf16_t*)A;
   auto Bb = (const bf16_t*)B;
   float* sl = S > 1 ? slabs : nullptr;
-  auto O = (bf16_t*)out;
 #define WG_LAUNCH(KERNEL, KS, NS, WM)                                                           \
   {                                                                                             \
     static bool attr = false;                                                                   \
@@ -305,8 +305,8 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
       attr = true;                                                                              \
     }                                                                                           \
     KERNEL<KS, NS, WM><<<ntiles * S, WM * 256, lds, st>>>(Ab, lda, Bb, ldb, M, N1, N2, t2,       \
-                                                          ntiles, chunk, sl, O, scale,          \
-                                                          accumulate);                          \
+                                                          ntiles, chunk, sl, out, scale,        \
+                                                          accumulate, out_f32);                 \
   }
   switch (wg_cfg()) {
     case 0: WG_LAUNCH(wgrad_kernel, 2, 4, 4) break;  // measured best on MI355X (16 waves, 122 VGPR)

@@ -52,7 +52,7 @@ class GradSink:
 
 
 def attach(param: torch.Tensor, view: torch.Tensor, listeners: list) -> GradSink | None:
-    if not ENABLED or view.dtype != torch.bfloat16 or not view.is_cuda:
+    if not ENABLED or view.dtype not in (torch.bfloat16, torch.float32) or not view.is_cuda:
         return None
     sink = GradSink(param, view, listeners)
     param._orion_sink = sink

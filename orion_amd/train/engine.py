@@ -1,4 +1,5 @@
-"""Training-step engine: flat bf16 arena + fused AdamW + optional RCCL DDP.
+"""Training-step engine: flat bf16 weight arena + fp32 gradient arena + fused AdamW +
+optional RCCL DDP.
 
 ``Trainer.step(batches)`` runs ``len(batches)`` micro-steps of forward and
 backward (gradient accumulation into the flat arena), reduces gradients across
@@ -67,13 +68,18 @@ class Trainer:
 
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float = 64.0, arena_dtype=None,
-                 graph: bool = False):
+                 graph: bool = False, grad_dtype=None):
         self.model = model
         self.cfg = optim or OptimConfig()
         dev = next(model.parameters()).device
         if arena_dtype is None:
             arena_dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
-        self.arena = FlatArena(model, dtype=arena_dtype)
+        if grad_dtype is None:
+            # fp32 gradients: micro-batch accumulation and the all-reduce keep fp32
+            # precision; ORION_GRAD_DTYPE=bf16 opts into the all-bf16 arena
+            grad_dtype = (torch.bfloat16 if os.environ.get("ORION_GRAD_DTYPE") == "bf16"
+                          else torch.float32)
+        self.arena = FlatArena(model, dtype=arena_dtype, grad_dtype=grad_dtype)
         self.opt = FlatAdamW(self.arena, lr=self.cfg.learning_rate,
                              betas=(self.cfg.beta1, self.cfg.beta2),
                              weight_decay=self.cfg.weight_decay, grad_clip=self.cfg.grad_clip)

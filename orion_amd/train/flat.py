@@ -12,6 +12,18 @@ buffer (what the GEMMs read) and their gradients into ONE contiguous buffer
   AdamW kernel can look up a parameter's weight-decay flag per 2048-element
   chunk with one byte load.
 
+Gradient dtype: the gradient arena is fp32 by default on the GPU (``Trainer``), so
+accumulation over micro-batches and the data-parallel all-reduce keep fp32
+precision (nanoGPT's fp32-gradient numerics) while the compute copy of the weights
+stays bf16.  A bf16 parameter cannot have an fp32 ``.grad``, so in that mode
+``p.grad`` is NOT bound to the arena: weight gradients reach their fp32 slice
+through the parameter's :class:`~orion_amd.ops.grad_sink.GradSink` (the GEMM /
+reduction kernel writes the slice directly, overwriting on the first write of a
+step and accumulating in its epilogue afterwards), and any gradient that still
+arrives through ``AccumulateGrad`` (tied weights, embeddings, ops without a sink)
+is folded into the slice by a post-accumulate hook and released.
+``grad_dtype=torch.bfloat16`` restores the all-bf16 arena.
+
 Parameters are laid out in *reverse* module-registration order, which is
 approximately the order backward produces their gradients, so the gradient
 buckets at the front of the arena fill first (see ``parallel/ddp.py``).
@@ -70,9 +82,12 @@ class FlatArena:
         # complete only after the LAST use's backward (the embedding, at the very end)
         self.shared = {id(p) for _, p in named if uses.get(id(p), 1) > 1}
         self.dtype = dtype
+        self.grad_dtype = grad_dtype
         self.device = device
         self.params = torch.zeros(off, dtype=dtype, device=device)
         self.grads = torch.zeros(off, dtype=grad_dtype, device=device)
+        # p.grad can alias the arena only when the dtypes agree (see module docstring)
+        self.bound = grad_dtype == dtype
         # per-ALIGN-chunk weight-decay flag (uint8) consumed by the fused AdamW kernel
         flags = torch.zeros(off // ALIGN, dtype=torch.uint8)
         for s in slots:
@@ -88,15 +103,32 @@ class FlatArena:
                 view.copy_(s.param.data)
                 self.init_fp32[s.offset: s.offset + s.numel].copy_(s.param.data.reshape(-1))
                 s.param.data = view
-                s.param.grad = self.grads[s.offset: s.offset + s.numel].view_as(s.param)
+                s.param.grad = self.grad_view(s).view_as(s.param) if self.bound else None
         # direct-to-arena weight gradients (ops/grad_sink.py); tied parameters excluded
         self.grad_listeners: list = []
         self.sinks = []
         for s in slots:
             if uses.get(id(s.param), 1) == 1:
-                sk = grad_sink.attach(s.param, s.param.grad, self.grad_listeners)
+                sk = grad_sink.attach(s.param, self.grad_view(s).view_as(s.param),
+                                      self.grad_listeners)
                 if sk is not None:
                     self.sinks.append(sk)
+        # unbound mode: fold AccumulateGrad results into the fp32 slice (registered before
+        # any reducer hook, so the reducer sees the folded slice)
+        self._fold_hooks = []
+        if not self.bound:
+            for s in slots:
+                self._fold_hooks.append(s.param.register_post_accumulate_grad_hook(
+                    self._make_fold(self.grad_view(s))))
+
+    @staticmethod
+    def _make_fold(dst):
+        def fold(p):
+            g = p.grad
+            if g is not None:
+                dst.add_(g.reshape(-1))
+                p.grad = None
+        return fold
 
     def param_view(self, slot: ParamSlot):
         return self.params[slot.offset: slot.offset + slot.numel]
@@ -116,8 +148,12 @@ class FlatArena:
         self.sinks = []
 
     def rebind_grads(self):
-        """Re-point ``p.grad`` at the arena (after anything replaced it)."""
+        """Re-point ``p.grad`` at the arena (after anything replaced it); unbound arenas
+        (fp32 gradients for bf16 parameters) keep ``p.grad`` empty instead."""
         for s in self.slots:
+            if not self.bound:
+                s.param.grad = None
+                continue
             g = s.param.grad
             if g is None or g.data_ptr() != self.grads[s.offset:].data_ptr():
                 s.param.grad = self.grads[s.offset: s.offset + s.numel].view_as(s.param)

@@ -84,3 +84,30 @@ def test_reference_gqa_and_rope_inverse():
     r = ref.rope(q, cos, sin)
     back = ref.rope(r, cos, -sin)
     assert torch.allclose(back, q, atol=1e-5)
+
+
+def test_fp32_grad_arena_for_bf16_params_folds_accumulate_grad():
+    """bf16 weights with an fp32 gradient arena: p.grad stays unbound, AccumulateGrad results
+    are folded into the fp32 slices, so A micro-batches sum in fp32 (here on the CPU, where
+    every gradient takes the AccumulateGrad path)."""
+    torch.manual_seed(0)
+    m1 = build_gpt2("gpt2-tiny", block_size=32).to(torch.bfloat16)
+    m2 = build_gpt2("gpt2-tiny", block_size=32).to(torch.bfloat16)
+    m2.load_state_dict(m1.state_dict())
+    arena = FlatArena(m1, dtype=torch.bfloat16, grad_dtype=torch.float32)
+    assert not arena.bound and arena.grads.dtype == torch.float32
+    batches = [(torch.randint(0, 50257, (2, 32)), torch.randint(0, 50257, (2, 32))) for _ in range(6)]
+    arena.zero_grad()
+    ref_acc = {n: torch.zeros(p.shape) for n, p in m2.named_parameters()}
+    for x, y in batches:
+        _, loss = m1(x, y)
+        (loss / len(batches)).backward()
+        m2.zero_grad(set_to_none=True)
+        _, l2 = m2(x, y)
+        (l2 / len(batches)).backward()
+        for n, p in m2.named_parameters():
+            ref_acc[n] += p.grad.float()
+    for s in arena.slots:
+        assert s.param.grad is None, s.name
+        got = arena.grads[s.offset:s.offset + s.numel].view(s.param.shape)
+        assert torch.allclose(got, ref_acc[s.name], atol=1e-6, rtol=1e-5), s.name
