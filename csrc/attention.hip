@@ -734,7 +734,13 @@ __global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p
     {
       const int qr0 = qbase + 16 * qgw * TPW;   // first q row of the wave's tiles
       int nks = BNK / 32;
-      if (CAUSAL) nks = min(nks, max(0, (qr0 + 16 * TPW - 1 + off - kt0) / 32 + 1));
+      if (CAUSAL) {
+        // last key of the workgroup any of these rows can see; negative = none (C division
+        // truncates toward zero, so the sign must be tested before dividing: with Tk > T a
+        // slice can start below the workgroup's first visible key)
+        const int last = qr0 + 16 * TPW - 1 + off - kt0;
+        nks = last < 0 ? 0 : min(nks, last / 32 + 1);
+      }
       f32x4 dq[TPW];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -1,0 +1,401 @@
+// Flash-attention backward as two atomic-free kernels (gfx950): dK/dV with the KEY on the
+// lane, dQ with the QUERY on the lane.  Deterministic (every output element is produced
+// by one workgroup in a fixed order), and the default at D = 128, where the fused kernels
+// of attention.hip (one pass producing dK, dV and fp32-atomic dQ partials) run out of
+// registers: a fused 8-wave / 256-key form needs ~370 VGPRs per lane, and the 4-wave v1
+// form runs at one wave per SIMD with the dQ fold through LDS on the critical path.
+//
+// The split recomputes S and dP once more (7 instead of 5 matmuls per (q, key) pair) but
+// each kernel keeps its accumulators and operand fragments in registers:
+//
+//   delta kernel   delta[q] = sum_d dO O                               (HBM-bound)
+//   kv kernel      per workgroup 32*NW keys, loop over 32-row query tiles (and the query
+//                  heads of its KV head):  S = Q K^T, dP = dO V^T (key on the lane, K/V
+//                  fragments in registers), P = exp2(c S - lse), dS = P (dP - delta),
+//                  dV^T += dO^T P, dK^T += Q^T dS (S/dP accumulators reused as B operands)
+//   dq kernel      the forward's structure: per workgroup 128 queries (32 per wave), K/V
+//                  tiles of 64 keys double-buffered in LDS; S^T = K Q^T and dP^T = V dO^T
+//                  (query on the lane: lse and delta are per-lane scalars), dS^T in place,
+//                  dQ^T += K^T dS^T with K^T by transposed LDS reads (ds_read_b64_tr_b16),
+//                  bf16 dQ written once -- no fp32 accumulator, no conversion pass.
+//
+// MFMA v_mfma_f32_32x32x16_bf16 throughout; LDS images and fragment helpers: mfma_lds.h.
+#include "common.h"
+#include "attn_params.h"
+#include "mfma_lds.h"
+
+namespace orion {
+
+// delta[b][h][t] = sum_d dO * O (D/8 lanes per row, 8 bf16 per lane)
+template <int D>
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* __restrict__ delta) {
+  constexpr int TPR = D / 8;
+  const long row = (blockIdx.x * 256L + threadIdx.x) / TPR;
+  const int sub = threadIdx.x % TPR;
+  const long nrows = (long)p.B * p.Hq * p.T;
+  float s = 0.f;
+  if (row < nrows) {
+    const long t = row % p.T, h = (row / p.T) % p.Hq, b = row / ((long)p.T * p.Hq);
+    const bf16x8 o = *reinterpret_cast<const bf16x8*>(p.o + b * p.o_sb + h * p.o_sh + t * p.o_st + sub * 8);
+    const bf16x8 d = *reinterpret_cast<const bf16x8*>(p.dout + b * p.do_sb + h * p.do_sh + t * p.do_st + sub * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += bf2f(o[j]) * bf2f(d[j]);
+  }
+#pragma unroll
+  for (int o2 = TPR / 2; o2 > 0; o2 >>= 1) s += __shfl_xor(s, o2, 64);
+  if (row < nrows && sub == 0) delta[row] = s;
+}
+
+// ============================================================================ dK / dV
+// NW waves x 32 keys per workgroup; query tiles of 32 rows double-buffered in LDS
+// (register staged: the next tile's loads are issued before this tile's MFMAs and written
+// after them).  One LDS barrier per tile.
+template <int D>
+__host__ __device__ constexpr int kv_waves() { return 4; }
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(kv_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_bwd_kv_kernel(AttnParams p) {
+  constexpr int NW = kv_waves<D>(), NT = NW * 64;
+  constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
+  constexpr int QT = BMQ * D;            // Q / dO tile elements
+  constexpr int NQC = BMQ * NCH;         // 16-byte chunks per Q (or dO) tile
+  constexpr int NSTQ = 2 * NQC / NT;     // chunks per thread per Q+dO stage
+  static_assert(NSTQ >= 1 && NSTQ * NT == 2 * NQC, "Q/dO staging must divide over the threads");
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* Qs = smem;                                        // [2][32][D]
+  bf16_t* Ds = Qs + 2 * QT;                                 // [2][32][D] (dO)
+  float* lse_s = reinterpret_cast<float*>(Ds + 2 * QT);     // [2][32]  -lse / c
+  float* del_s = lse_s + 2 * BMQ;                           // [2][32]  -delta
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int BHk = p.B * p.Hkv;
+  const int kt = blockIdx.x / BHk;  // small kt = most work under the causal mask: first
+  const int bh = blockIdx.x % BHk;
+  const int b = bh / p.Hkv, hk = bh % p.Hkv;
+  const int rep = p.Hq / p.Hkv;
+  const int kt0 = kt * BNK, kw0 = kt0 + wv * 32, mykey = kw0 + l32;
+  const int off = p.Tk - p.T;
+  const float c = p.scale_log2, inv_c = 1.f / p.scale_log2;
+
+  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
+  // K / V fragments of this wave's 32 keys: B operands of S and dP for every query tile
+  bf16x8 kf[D / 16], vf[D / 16];
+  {
+    const long key = min(mykey, p.Tk - 1);
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ks * 16 + 8 * h32);
+    }
+  }
+  f32x16 dka[NDB], dva[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) { dka[db] = zero16(); dva[db] = zero16(); }
+
+  const int qlo = CAUSAL ? max(0, kt0 - off) : 0;  // first query row that sees any key here
+  const int qi0 = qlo / BMQ;
+  const int nqi = (p.T + BMQ - 1) / BMQ;
+  const int iters_per_head = max(0, nqi - qi0);
+  const int total = iters_per_head * rep;
+
+  bf16x8 qdst[NSTQ];
+  float lse_r = 0.f, del_r = 0.f;
+  auto gload = [&](int it) {
+    const int hq = hk * rep + it / iters_per_head;
+    const int qbase = (qi0 + it % iters_per_head) * BMQ;
+    const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
+    const bf16_t* Db = p.dout + b * p.do_sb + hq * p.do_sh;
+    if constexpr (NSTQ >= 2) {
+#pragma unroll
+      for (int i = 0; i < NSTQ / 2; ++i) {
+        const int cc = tid + i * NT, row = cc / NCH, ch = cc % NCH;
+        const long q = min(qbase + row, p.T - 1);
+        qdst[i] = *reinterpret_cast<const bf16x8*>(Qb + q * p.q_st + ch * 8);
+        qdst[NSTQ / 2 + i] = *reinterpret_cast<const bf16x8*>(Db + q * p.do_st + ch * 8);
+      }
+    } else {  // one chunk per thread: the first NQC threads take Q, the rest dO
+      const int isd = tid >= NQC, w = tid - isd * NQC;
+      const long q = min(qbase + w / NCH, p.T - 1);
+      const bf16_t* src = isd ? Db + q * p.do_st : Qb + q * p.q_st;
+      qdst[0] = *reinterpret_cast<const bf16x8*>(src + (w % NCH) * 8);
+    }
+    if (tid < BMQ) {
+      const long q = min(qbase + tid, p.T - 1);
+      const long r = ((long)b * p.Hq + hq) * p.T + q;
+      lse_r = p.lse[r];
+      del_r = p.delta[r];
+    }
+  };
+  auto swrite = [&](int buf) {
+    if constexpr (NSTQ >= 2) {
+#pragma unroll
+      for (int i = 0; i < NSTQ / 2; ++i) {
+        const int cc = tid + i * NT, o = loff<D>(cc / NCH, (cc % NCH) * 8);
+        *reinterpret_cast<bf16x8*>(Qs + buf * QT + o) = qdst[i];
+        *reinterpret_cast<bf16x8*>(Ds + buf * QT + o) = qdst[NSTQ / 2 + i];
+      }
+    } else {
+      const int isd = tid >= NQC, w = tid - isd * NQC;
+      *reinterpret_cast<bf16x8*>((isd ? Ds : Qs) + buf * QT + loff<D>(w / NCH, (w % NCH) * 8)) = qdst[0];
+    }
+    if (tid < BMQ) {  // row constants as the initial S / dP accumulators
+      lse_s[buf * BMQ + tid] = -lse_r * inv_c;
+      del_s[buf * BMQ + tid] = -del_r;
+    }
+  };
+
+  if (total > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    const int qbase = (qi0 + it % iters_per_head) * BMQ;
+    if (it + 1 < total) gload(it + 1);
+    const bf16_t* Qc = Qs + buf * QT;
+    const bf16_t* Dc = Ds + buf * QT;
+    // wave-uniform: this wave's keys are all above every query of the tile
+    const bool active = !CAUSAL || (qbase + BMQ - 1 + off >= kw0);
+    if (active) {
+      // S - lse/c and dP - delta straight out of the MFMA chains (row constants preloaded)
+      f32x16 s, dp;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 L = *reinterpret_cast<const f32x4*>(lse_s + buf * BMQ + 8 * g4 + 4 * h32);
+        const f32x4 Dl = *reinterpret_cast<const f32x4*>(del_s + buf * BMQ + 8 * g4 + 4 * h32);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { s[4 * g4 + j] = L[j]; dp[4 * g4 + j] = Dl[j]; }
+      }
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const int o = loff<D>(l32, ks * 16 + 8 * h32);
+        s = mfma32(lds_b128(Qc, o), kf[ks], s);
+        dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
+      }
+      // P and dS in place: row q = qbase + (r&3)+8(r>>2)+4*h32, column = mykey
+      const bool need_mask = (CAUSAL && (qbase + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
+                             (qbase + BMQ > p.T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = __builtin_amdgcn_exp2f(s[r] * c);
+        if (need_mask) {
+          const int q = qbase + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          if (mykey >= p.Tk || q >= p.T || (CAUSAL && mykey > q + off)) pv = 0.f;
+        }
+        s[r] = pv;
+        dp[r] = pv * dp[r];  // dS / scale: the scale is applied to dK once at the end
+      }
+      bf16x8 pb[2], sb[2];
+      pb[0] = acc_to_frag(s, 0);
+      pb[1] = acc_to_frag(s, 1);
+      sb[0] = acc_to_frag(dp, 0);
+      sb[1] = acc_to_frag(dp, 1);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          dva[db] = mfma32(tr_frag<D>(Dc, 16 * s2 + 4 * h32, db * 32, lane, 8), pb[s2], dva[db]);
+          dka[db] = mfma32(tr_frag<D>(Qc, 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
+        }
+      }
+    }
+    if (it + 1 < total) swrite(buf ^ 1);
+    __syncthreads();
+  }
+
+  // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
+  if (mykey < p.Tk) {
+    bf16_t* dKb = p.dk + b * p.dk_sb + hk * p.dk_sh + (long)mykey * p.dk_st;
+    bf16_t* dVb = p.dv + b * p.dv_sb + hk * p.dv_sh + (long)mykey * p.dv_st;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 k4, v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          k4[j] = f2bf(dka[db][4 * g4 + j] * p.scale);
+          v4[j] = f2bf(dva[db][4 * g4 + j]);
+        }
+        *reinterpret_cast<bf16x4*>(dKb + db * 32 + 8 * g4 + 4 * h32) = k4;
+        *reinterpret_cast<bf16x4*>(dVb + db * 32 + 8 * g4 + 4 * h32) = v4;
+      }
+  }
+}
+
+// ============================================================================ dQ
+// One 256-thread workgroup = 4 waves x 32 queries; key tiles of 64 double-buffered in LDS.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
+  constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int BH = p.B * p.Hq;
+  const int nqt = (p.T + BM - 1) / BM;
+  const int bh = blockIdx.x % BH;
+  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) tiles launch first
+  const int b = bh / p.Hq, hq = bh % p.Hq, hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qt * BM, qw0 = q0 + wv * 32, myq = qw0 + l32;
+  const int off = p.Tk - p.T;
+  const float c = p.scale_log2;
+
+  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
+
+  // Q and dO fragments of this wave's 32 queries: B operands of S^T = K Q^T, dP^T = V dO^T
+  bf16x8 qf[D / 16], df[D / 16];
+  float L, dl;
+  {
+    const int qr = min(myq, p.T - 1);
+    const bf16_t* Qr = p.q + b * p.q_sb + hq * p.q_sh + (long)qr * p.q_st;
+    const bf16_t* Dr = p.dout + b * p.do_sb + hq * p.do_sh + (long)qr * p.do_st;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Qr + ks * 16 + 8 * h32);
+      df[ks] = *reinterpret_cast<const bf16x8*>(Dr + ks * 16 + 8 * h32);
+    }
+    const long r = ((long)b * p.Hq + hq) * p.T + qr;
+    L = p.lse[r];
+    dl = p.delta[r];
+  }
+  const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
+  const int ntiles = (kend + BN - 1) / BN;
+
+  bf16x8 kst[NST], vst[NST];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+      const long key = min(t * BN + row, p.Tk - 1);
+      kst[i] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ch * 8);
+      vst[i] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ch * 8);
+    }
+  };
+  auto swrite = [&](int buf) {
+    bf16_t* Ks = smem + buf * 2 * TILE;
+    bf16_t* Vs = Ks + TILE;
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+      const int o = loff<D>(row, ch * 8);
+      *reinterpret_cast<bf16x8*>(Ks + o) = kst[i];
+      *reinterpret_cast<bf16x8*>(Vs + o) = vst[i];
+    }
+  };
+
+  f32x16 dq[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) dq[db] = zero16();
+
+  if (ntiles > 0) {
+    gload(0);
+    swrite(0);
+  }
+  // retire the prologue loads with a wait the compiler can see (see attn_fwd_kernel)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    const bf16_t* Ks = smem + (t & 1) * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int k0 = t * BN + kb * 32;
+      if (CAUSAL && k0 > qw0 + 31 + off) continue;  // wave-uniform: block fully masked
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const int o = loff<D>(kb * 32 + l32, ks * 16 + 8 * h32);
+        s = mfma32(lds_b128(Ks, o), qf[ks], s);
+        dp = mfma32(lds_b128(Vs, o), df[ks], dp);
+        if constexpr (D == 128) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
+      }
+      // S^T / dP^T: row = key k0 + (r&3)+8(r>>2)+4*h32, column = this lane's query
+      const bool need_mask = (CAUSAL && (k0 + 31 > qw0 + off)) || (k0 + 32 > p.Tk);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c, -L));
+        if (need_mask) {
+          const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          if (key >= p.Tk || (CAUSAL && key > myq + off)) pv = 0.f;
+        }
+        dp[r] = pv * (dp[r] - dl);  // dS^T / scale
+      }
+      const bf16x8 ds0 = acc_to_frag(dp, 0), ds1 = acc_to_frag(dp, 1);
+      // dQ^T += K^T dS^T: A = K^T by transposed reads of the K image (key order permuted
+      // within each 16-key step exactly as the accumulator-as-operand dS^T fragment)
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        dq[db] = mfma32(tr_frag<D>(Ks, kb * 32 + 4 * h32, db * 32, lane, 8), ds0, dq[db]);
+        dq[db] = mfma32(tr_frag<D>(Ks, kb * 32 + 16 + 4 * h32, db * 32, lane, 8), ds1, dq[db]);
+      }
+    }
+    if (t + 1 < ntiles) swrite((t + 1) & 1);
+    __syncthreads();
+  }
+
+  if (myq < p.T) {
+    bf16_t* Qo = p.dq + b * p.dq_sb + hq * p.dq_sh + (long)myq * p.dq_st;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(dq[db][4 * g4 + j] * p.scale);
+        *reinterpret_cast<bf16x4*>(Qo + db * 32 + 8 * g4 + 4 * h32) = v4;
+      }
+  }
+}
+
+}  // namespace orion
+
+using namespace orion;
+
+extern "C++" {
+
+static size_t kv_lds(int D) { return (size_t)2 * 2 * 32 * D * 2 + 4 * 32 * 4; }
+static size_t dq_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
+
+template <int D, bool CAUSAL>
+static void split_attrs() {
+  static bool done = false;
+  if (!done) {
+    hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, CAUSAL>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(D));
+    hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
+    done = true;
+  }
+}
+
+// delta (caller-allocated [B][Hq][T] fp32) then dK/dV and dQ; p.dq / dk / dv are bf16
+// outputs (strided views allowed).  kv and dq launches are independent after delta.
+int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
+  const long rows = (long)p.B * p.Hq * p.T;
+  const int pre_grid = (int)((rows * (D / 8) + 255) / 256);
+  AttnParams q = p;
+  q.delta = delta;
+  const int kv_grid = ((p.Tk + 32 * 4 - 1) / (32 * 4)) * p.B * p.Hkv;
+  const int dq_grid = ((p.T + 127) / 128) * p.B * p.Hq;
+#define SPLIT(DD, CC)                                                                   \
+  attn_delta_kernel<DD><<<pre_grid, 256, 0, st>>>(p, delta);                            \
+  split_attrs<DD, CC>();                                                                \
+  attn_bwd_kv_kernel<DD, CC><<<kv_grid, kv_waves<DD>() * 64, kv_lds(DD), st>>>(q);      \
+  attn_bwd_dq_kernel<DD, CC><<<dq_grid, 256, dq_lds(DD), st>>>(q);
+  if (D == 64) {
+    if (causal) { SPLIT(64, true) } else { SPLIT(64, false) }
+  } else if (D == 128) {
+    if (causal) { SPLIT(128, true) } else { SPLIT(128, false) }
+  } else {
+    return -1;
+  }
+#undef SPLIT
+  return (int)hipGetLastError();
+}
+
+}  // extern "C++"

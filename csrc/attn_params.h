@@ -25,7 +25,9 @@ struct AttnParams {
   long dk_sb, dk_st, dk_sh;
   unsigned short* dv;
   long dv_sb, dv_st, dv_sh;
-  int flags;  // diagnostic bits (0 in production): 1 = skip dQ atomics
+  unsigned short* dq;  // bf16 dQ (split backward: written directly, no fp32 accumulator)
+  long dq_sb, dq_st, dq_sh;
+  int flags;  // 1 = skip dQ atomics (diagnostic), 4 = deterministic (split backward), 8 = fused
 };
 
 }  // namespace orion

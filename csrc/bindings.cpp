@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <tuple>
 
 #include "attn_params.h"
@@ -49,6 +50,7 @@ int orion_rope(const void*, long, long, long, void*, long, long, long, const flo
 int orion_attn_fwd(const orion::AttnParams&, int, bool, hipStream_t);
 int orion_attn_bwd(const orion::AttnParams&, int, bool, float*, hipStream_t);
 int orion_attn_dq_convert(const float*, void*, long, long, long, int, int, int, int, hipStream_t);
+int orion_attn_bwd_split(const orion::AttnParams&, int, bool, float*, hipStream_t);
 
 namespace {
 
@@ -534,6 +536,23 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
   return {o, lse};
 }
 
+// Backward form: "split" (csrc/attn_bwd_split.hip: dK/dV and dQ kernels, no atomics,
+// deterministic) or "fused" (csrc/attention.hip: one pass, fp32-atomic dQ).  Split is the
+// default (MI355X: 0.632 vs 0.722 ms at B64 T1024 H12 D64, 3.39 vs 4.46 ms at B4 T4096
+// H32/8 D128); flags bit 2 (deterministic) forces split, bit 3 forces fused; otherwise
+// ORION_ATTN_BWD = split | v1 | v2 overrides the default.
+bool attn_bwd_use_split(int D, int64_t flags) {
+  if (flags & 4) return true;
+  if (flags & 8) return false;  // force the fused form (A/B tests)
+  static int env = -1;  // -1 unread, 0 none, 1 split, 2 fused
+  if (env < 0) {
+    const char* e = getenv("ORION_ATTN_BWD");
+    env = !e ? 0 : (strcmp(e, "split") == 0 ? 1 : 2);
+  }
+  if (env) return env == 1;
+  return true;  // measured faster at both head dims (docs/PERFORMANCE.md)
+}
+
 // dq/dk/dv: preallocated outputs (may be strided views of one packed buffer)
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
               const Tensor& o, const Tensor& lse, bool causal, double scale, Tensor dq, Tensor dk,
@@ -553,14 +572,21 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   p.dout = (const unsigned short*)dout.data_ptr();
   p.do_sb = dout.stride(0); p.do_st = dout.stride(1); p.do_sh = dout.stride(2);
   auto fopts = q.options().dtype(at::kFloat);
-  auto dq_acc = at::empty({p.B, p.Hq, p.T, D}, fopts);
   auto delta = at::empty({p.B, p.Hq, p.T}, fopts);
-  p.dq_acc = dq_acc.data_ptr<float>();
   p.dk = (unsigned short*)dk.data_ptr();
   p.dk_sb = dk.stride(0); p.dk_st = dk.stride(1); p.dk_sh = dk.stride(2);
   p.dv = (unsigned short*)dv.data_ptr();
   p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
   p.flags = (int)flags;
+  if (attn_bwd_use_split(D, flags)) {
+    p.dq = (unsigned short*)dq.data_ptr();
+    p.dq_sb = dq.stride(0); p.dq_st = dq.stride(1); p.dq_sh = dq.stride(2);
+    check_launch(orion_attn_bwd_split(p, D, causal, delta.data_ptr<float>(), cur_stream()),
+                 "attn_bwd_split");
+    return;
+  }
+  auto dq_acc = at::empty({p.B, p.Hq, p.T, D}, fopts);
+  p.dq_acc = dq_acc.data_ptr<float>();
   check_launch(orion_attn_bwd(p, D, causal, delta.data_ptr<float>(), cur_stream()), "attn_bwd");
   check_launch(orion_attn_dq_convert(dq_acc.data_ptr<float>(), dq.data_ptr(), dq.stride(0),
                                      dq.stride(1), dq.stride(2), p.B, p.Hq, p.T, D, cur_stream()),

@@ -7,10 +7,22 @@ buffer, so there is no split/transpose/concat around the kernels.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from ._ext import C
+
+
+def deterministic() -> bool:
+    """Bitwise-reproducible attention gradients: ``ORION_DETERMINISTIC=1`` or
+    ``torch.use_deterministic_algorithms(True)`` select the split backward
+    (csrc/attn_bwd_split.hip: no atomics) at every head dim."""
+    return os.environ.get("ORION_DETERMINISTIC") == "1" or torch.are_deterministic_algorithms_enabled()
+
+
+def _bwd_flags() -> int:
+    return 4 if deterministic() else 0
 
 
 class _FlashQKV(torch.autograd.Function):
@@ -37,7 +49,7 @@ class _FlashQKV(torch.autograd.Function):
         d5 = dqkv.view(B, T, 3, n_head, D)
         do4 = do.contiguous().view(B, T, n_head, D)
         C().attn_bwd(do4, v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], o, lse, causal, scale,
-                     d5[:, :, 0], d5[:, :, 1], d5[:, :, 2])
+                     d5[:, :, 0], d5[:, :, 1], d5[:, :, 2], _bwd_flags())
         return dqkv, None, None
 
 
@@ -62,7 +74,7 @@ class _Flash(torch.autograd.Function):
         dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
         dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
         dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
-        C().attn_bwd(do.contiguous(), q, k, v, o, lse, causal, scale, dq, dk, dv)
+        C().attn_bwd(do.contiguous(), q, k, v, o, lse, causal, scale, dq, dk, dv, _bwd_flags())
         return dq, dk, dv, None
 
 
@@ -99,7 +111,8 @@ class _RopeFlashPacked(torch.autograd.Function):
         n_q, n_kv, pos0, scale = ctx.meta
         dqkv = torch.empty_like(qkv)
         C().attn_bwd(do.contiguous(), qk[:, :, :n_q], qk[:, :, n_q:], qkv[:, :, n_q + n_kv:], o, lse,
-                     True, scale, dqkv[:, :, :n_q], dqkv[:, :, n_q:n_q + n_kv], dqkv[:, :, n_q + n_kv:])
+                     True, scale, dqkv[:, :, :n_q], dqkv[:, :, n_q:n_q + n_kv], dqkv[:, :, n_q + n_kv:],
+                     _bwd_flags())
         C().rope_(dqkv[:, :, :n_q + n_kv], cos, sin, pos0, -1.0)
         return dqkv, None, None, None, None, None
 

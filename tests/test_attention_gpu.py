@@ -1,0 +1,105 @@
+"""Attention backward forms on the GPU vs the fp32 PyTorch reference (ops/reference.py):
+the fused kernel (fp32-atomic dQ, csrc/attention.hip) and the split kernels (dK/dV + dQ, no
+atomics, csrc/attn_bwd_split.hip), determinism of the split form, the long-context
+Llama-7B attention shape (T = 4096, GQA 32/8, D = 128) and Tk != T (bottom-right causal)."""
+import math
+
+import pytest
+import torch
+
+from orion_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+FUSED, SPLIT = 8, 4  # attn_bwd flags (csrc/bindings.cpp)
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _C():
+    from orion_amd.ops._ext import C, load_ext
+    load_ext(required=True)
+    return C()
+
+
+def _run(q, k, v, do, causal, flags):
+    C = _C()
+    scale = 1.0 / math.sqrt(q.shape[-1])
+    o, lse = C.attn_fwd(q, k, v, causal, scale)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    C.attn_bwd(do, q, k, v, o, lse, causal, scale, dq, dk, dv, flags)
+    return o, dq, dk, dv
+
+
+def _ref(q, k, v, do, causal):
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o = ref.attention(qr, kr, vr, causal).float()
+    o.backward(do.float())
+    return o, qr.grad, kr.grad, vr.grad
+
+
+def _inputs(B, T, Tk, Hq, Hkv, D, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    mk = lambda *s: torch.randn(*s, device=DEV, dtype=torch.bfloat16, generator=g)
+    return mk(B, T, Hq, D), mk(B, Tk, Hkv, D), mk(B, Tk, Hkv, D), mk(B, T, Hq, D)
+
+
+@pytest.mark.parametrize("form", [FUSED, SPLIT])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+def test_backward_forms_match_reference(form, D, causal):
+    q, k, v, do = _inputs(2, 320, 320, 4, 2, D)
+    got = _run(q, k, v, do, causal, form)
+    want = _ref(q, k, v, do, causal)
+    for name, a, b in zip(("o", "dq", "dk", "dv"), got, want):
+        assert rel_err(a, b) < 3e-2, (name, rel_err(a, b))
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_split_backward_is_deterministic(D):
+    q, k, v, do = _inputs(2, 512, 512, 8, 2, D, seed=3)
+    a = _run(q, k, v, do, True, SPLIT)
+    b = _run(q, k, v, do, True, SPLIT)
+    for x, y in zip(a[1:], b[1:]):
+        assert torch.equal(x, y)
+
+
+def test_deterministic_switch_routes_ops_to_split(monkeypatch):
+    from orion_amd import ops
+    from orion_amd.ops import flash_attn
+    monkeypatch.setenv("ORION_DETERMINISTIC", "1")
+    assert flash_attn._bwd_flags() == SPLIT
+    q, k, v, do = _inputs(1, 256, 256, 4, 4, 64, seed=5)
+    grads = []
+    for _ in range(2):
+        qq, kk, vv = (t.clone().requires_grad_() for t in (q, k, v))
+        ops.attention(qq, kk, vv, causal=True).backward(do)
+        grads.append((qq.grad, kk.grad, vv.grad))
+    for x, y in zip(*grads):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("form", [FUSED, SPLIT])
+def test_long_context_llama7b_attention_shape(form):
+    """BASELINE config 4's attention: T = 4096, 32 query heads on 8 KV heads, D = 128."""
+    q, k, v, do = _inputs(1, 4096, 4096, 32, 8, 128, seed=1)
+    got = _run(q, k, v, do, True, form)
+    want = _ref(q, k, v, do, True)
+    for name, a, b in zip(("o", "dq", "dk", "dv"), got, want):
+        assert rel_err(a, b) < 3e-2, (name, rel_err(a, b))
+
+
+@pytest.mark.parametrize("form", [FUSED, SPLIT])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+def test_cross_length_tk_ne_t(form, D, causal):
+    """Tk > T (a query block at the end of a longer key sequence, causal bottom-right)."""
+    q, k, v, do = _inputs(2, 192, 328, 4, 2, D, seed=2)
+    got = _run(q, k, v, do, causal, form)
+    want = _ref(q, k, v, do, causal)
+    for name, a, b in zip(("o", "dq", "dk", "dv"), got, want):
+        assert rel_err(a, b) < 3e-2, (name, rel_err(a, b))
