@@ -1,17 +1,19 @@
 // Flash-attention backward as two atomic-free kernels (gfx950): dK/dV with the KEY on the
 // lane, dQ with the QUERY on the lane.  Deterministic (every output element is produced
-// by one workgroup in a fixed order), and the default at D = 128, where the fused kernels
-// of attention.hip (one pass producing dK, dV and fp32-atomic dQ partials) run out of
-// registers: a fused 8-wave / 256-key form needs ~370 VGPRs per lane, and the 4-wave v1
-// form runs at one wave per SIMD with the dQ fold through LDS on the critical path.
+// by one workgroup in a fixed order) and the default backward: faster than the fused
+// kernels of attention.hip (one pass producing dK, dV and fp32-atomic dQ partials) at both
+// head dims -- at D = 128 those run out of registers (a fused 8-wave / 256-key form needs
+// ~370 VGPRs per lane; the 4-wave v1 form runs at one wave per SIMD with the dQ fold
+// through LDS on the critical path), at D = 64 the dQ atomics floor them.
 //
 // The split recomputes S and dP once more (7 instead of 5 matmuls per (q, key) pair) but
 // each kernel keeps its accumulators and operand fragments in registers:
 //
 //   delta kernel   delta[q] = sum_d dO O                               (HBM-bound)
 //   kv kernel      per workgroup 32*NW keys, loop over 32-row query tiles (and the query
-//                  heads of its KV head):  S = Q K^T, dP = dO V^T (key on the lane, K/V
-//                  fragments in registers), P = exp2(c S - lse), dS = P (dP - delta),
+//                  heads of its KV head):  S = Q K^T, dP = dO V^T (key on the lane, V
+//                  fragments in registers, K in registers or an LDS image),
+//                  P = exp2(c S - lse), dS = P (dP - delta),
 //                  dV^T += dO^T P, dK^T += Q^T dS (S/dP accumulators reused as B operands)
 //   dq kernel      the forward's structure: per workgroup 128 queries (32 per wave), K/V
 //                  tiles of 64 keys double-buffered in LDS; S^T = K Q^T and dP^T = V dO^T
@@ -49,20 +51,25 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* __
 // ============================================================================ dK / dV
 // NW waves x 32 keys per workgroup; query tiles of 32 rows double-buffered in LDS
 // (register staged: the next tile's loads are issued before this tile's MFMAs and written
-// after them).  One LDS barrier per tile.
+// after them).  One LDS barrier per tile.  Two workgroups per CU (two waves per SIMD, so
+// one wave's MFMAs overlap the other's softmax / LDS phase): at D = 128 that fits the
+// 256-register budget only with the K fragments read from an LDS image per query tile
+// (KLDS) instead of held in registers (25 spilled registers otherwise).
 template <int D>
 __host__ __device__ constexpr int kv_waves() { return 4; }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(kv_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_bwd_kv_kernel(AttnParams p) {
+__global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
   constexpr int NW = kv_waves<D>(), NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
   constexpr int QT = BMQ * D;            // Q / dO tile elements
   constexpr int NQC = BMQ * NCH;         // 16-byte chunks per Q (or dO) tile
   constexpr int NSTQ = 2 * NQC / NT;     // chunks per thread per Q+dO stage
+  constexpr bool KLDS = D == 128;        // K fragments from an LDS image, not registers
   static_assert(NSTQ >= 1 && NSTQ * NT == 2 * NQC, "Q/dO staging must divide over the threads");
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Qs = smem;                                        // [2][32][D]
+  bf16_t* Ks = smem;                                        // [BNK][D] (KLDS only)
+  bf16_t* Qs = Ks + (KLDS ? BNK * D : 0);                   // [2][32][D]
   bf16_t* Ds = Qs + 2 * QT;                                 // [2][32][D] (dO)
   float* lse_s = reinterpret_cast<float*>(Ds + 2 * QT);     // [2][32]  -lse / c
   float* del_s = lse_s + 2 * BMQ;                           // [2][32]  -delta
@@ -81,13 +88,21 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_bw
   const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
   // K / V fragments of this wave's 32 keys: B operands of S and dP for every query tile
-  bf16x8 kf[D / 16], vf[D / 16];
+  bf16x8 kf[KLDS ? 1 : D / 16], vf[D / 16];
   {
     const long key = min(mykey, p.Tk - 1);
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
-      kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
+      if constexpr (!KLDS) kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
       vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ks * 16 + 8 * h32);
+    }
+  }
+  if constexpr (KLDS) {
+    for (int cidx = tid; cidx < BNK * NCH; cidx += NT) {
+      const int row = cidx / NCH, ch = cidx % NCH;
+      const long key = min(kt0 + row, p.Tk - 1);
+      *reinterpret_cast<bf16x8*>(Ks + loff<D>(row, ch * 8)) =
+          *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ch * 8);
     }
   }
   f32x16 dka[NDB], dva[NDB];
@@ -172,8 +187,12 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_bw
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
         const int o = loff<D>(l32, ks * 16 + 8 * h32);
-        s = mfma32(lds_b128(Qc, o), kf[ks], s);
+        bf16x8 kfr;
+        if constexpr (KLDS) kfr = lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
+        else kfr = kf[ks];
+        s = mfma32(lds_b128(Qc, o), kfr, s);
         dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
+        if constexpr (KLDS) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
       }
       // P and dS in place: row q = qbase + (r&3)+8(r>>2)+4*h32, column = mykey
       const bool need_mask = (CAUSAL && (qbase + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
@@ -358,7 +377,9 @@ using namespace orion;
 
 extern "C++" {
 
-static size_t kv_lds(int D) { return (size_t)2 * 2 * 32 * D * 2 + 4 * 32 * 4; }
+static size_t kv_lds(int D) {
+  return (size_t)2 * 2 * 32 * D * 2 + 4 * 32 * 4 + (D == 128 ? (size_t)32 * 4 * D * 2 : 0);
+}
 static size_t dq_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
 
 template <int D, bool CAUSAL>
