@@ -51,6 +51,8 @@ int orion_attn_fwd(const orion::AttnParams&, int, bool, hipStream_t);
 int orion_attn_bwd(const orion::AttnParams&, int, bool, float*, hipStream_t);
 int orion_attn_dq_convert(const float*, void*, long, long, long, int, int, int, int, hipStream_t);
 int orion_attn_bwd_split(const orion::AttnParams&, int, bool, float*, hipStream_t);
+int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, void*, long,
+               const void*, void*, long, const void*, long, hipStream_t);
 
 namespace {
 
@@ -371,6 +373,55 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& sca
 
 int64_t wgrad_splits(int64_t M, int64_t N1, int64_t N2) { return orion_wgrad_splits(M, N1, N2); }
 
+// ------------------------------------------------------------------ GEMM (csrc/gemm.hip)
+// out (..., N) = x (..., K) . op(w) with op(w) = w^T for w (N, K) [w_kmajor = false, the
+// nn.Linear forward] or w for w (K, N) [w_kmajor = true, the input gradient], and a fused
+// epilogue: 0 store, 1 + bias, 2 + bias then GELU (returns (a, gelu(a))), 3 times
+// GELU'(pre).  Returns (out, out2); out2 is undefined unless epi == 2.
+std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor, int64_t epi,
+                                const c10::optional<Tensor>& bias, const c10::optional<Tensor>& pre) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemm: w must be a contiguous 2-D tensor");
+  TORCH_CHECK(x.stride(-1) == 1, "gemm: x rows must be contiguous");
+  const int64_t K = x.size(-1);
+  TORCH_CHECK(K == (w_kmajor ? w.size(0) : w.size(1)), "gemm: reduction dims differ");
+  const int64_t N = w_kmajor ? w.size(1) : w.size(0);
+  auto x2 = x.reshape({-1, K});
+  TORCH_CHECK(x2.stride(1) == 1, "gemm: x must flatten to rows");
+  const int64_t M = x2.size(0);
+  TORCH_CHECK(M < (1LL << 31) && N < (1 << 30), "gemm: shape too large");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  auto out = at::empty(sizes, x.options());
+  Tensor out2, bc, pc;
+  const void* bp = nullptr;
+  const void* pp = nullptr;
+  long ldp = 0;
+  if (epi == 1 || epi == 2) {
+    TORCH_CHECK(bias.has_value() && bias->defined(), "gemm: epilogue needs a bias");
+    check_bf16(*bias, "bias");
+    bc = bias->contiguous();
+    TORCH_CHECK(bc.numel() == N, "gemm: bias must have N elements");
+    bp = bc.data_ptr();
+  }
+  if (epi == 2) out2 = at::empty(sizes, x.options());
+  if (epi == 3) {
+    TORCH_CHECK(pre.has_value() && pre->defined(), "gemm: GELU backward needs the pre-activation");
+    check_bf16(*pre, "pre");
+    pc = pre->reshape({-1, N});
+    TORCH_CHECK(pc.size(0) == M && pc.stride(1) == 1, "gemm: pre must be (M, N) with unit column stride");
+    pp = pc.data_ptr();
+    ldp = pc.stride(0);
+  }
+  check_launch(orion_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), (int)M, (int)N,
+                          (int)K, w_kmajor ? 1 : 0, (int)epi, out.data_ptr(), N, bp,
+                          out2.defined() ? out2.data_ptr() : nullptr, N, pp, ldp, cur_stream()),
+               "gemm");
+  return {out, out2};
+}
+
 // ------------------------------------------------------------------ optimizer
 void grad_sumsq(const Tensor& g, Tensor out) {
   check_grad_out(g, "grads");
@@ -610,6 +661,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("wgrad_into(Tensor dy, Tensor x, Tensor? scale, Tensor(a!) out, bool accumulate, int splits=0) -> ()");
   m.def("wgrad_splits(int M, int N1, int N2) -> int", &wgrad_splits);  // host-only helper
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
+  m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
@@ -635,6 +687,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("wgrad", &wgrad);
   m.impl("wgrad_into", &wgrad_into);
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
+  m.impl("gemm", &gemm);
   m.impl("grad_sumsq", &grad_sumsq);
   m.impl("adamw_flat", &adamw_flat);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);

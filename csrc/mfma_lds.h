@@ -27,6 +27,13 @@ ORION_DEVICE int loff(int row, int col) {
   return row * D + ((((col >> 3) ^ swz<D>(row))) << 3) + (col & 7);
 }
 
+// [rows][32] bf16 image (64-byte rows, four 16-byte chunks): chunk c of row r at
+// c ^ ((r >> 2) & 3).  ds_read_b128 of 32 consecutive rows at one chunk is conflict-free:
+// each 16-lane group of the instruction covers 16 distinct (r & 3, slot) pairs.
+ORION_DEVICE int loff32(int row, int col) {
+  return row * 32 + ((((col >> 3) ^ (row >> 2)) & 3) << 3) + (col & 7);
+}
+
 ORION_DEVICE bf16x8 lds_b128(const bf16_t* base, int off) {
   return *reinterpret_cast<const bf16x8*>(base + off);
 }
@@ -75,6 +82,63 @@ ORION_DEVICE bf16x8 tr_frag(const bf16_t* img, int rbase, int cbase, int lane, i
   const int row = rbase + (i >> 2);
   const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
   return cat8(lds_tr(img, loff<D>(row, col)), lds_tr(img, loff<D>(row + rstep, col)));
+}
+
+// ---------------------------------------------------------------- LDS-DMA and asm LDS reads
+// 16 bytes per lane global -> LDS (global_load_lds_dwordx4): the LDS destination is the
+// wave-uniform base `l` + 16 * lane; the per-lane SOURCE address carries any swizzle.
+ORION_DEVICE void glds16(const bf16_t* g, bf16_t* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+ORION_DEVICE unsigned lds_addr(const bf16_t* lds, int elem) {
+  return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(lds + elem));
+}
+
+// LDS reads as inline asm: reads the compiler cannot see, so its waitcnt pass does not
+// drain an in-flight LDS-DMA ring (vmcnt(0)) before them, as it does before the builtin
+// forms.  Completion is waited for by hand (s_waitcnt lgkmcnt(N)).
+ORION_DEVICE bf16x4 tr_read(const bf16_t* lds, int elem) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr(lds, elem)));
+  return r;
+}
+
+ORION_DEVICE bf16x8 b128_read(const bf16_t* lds, int elem) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(lds_addr(lds, elem)));
+  return r;
+}
+
+// tr_frag (above) on the asm read, [rows][128] image: element j of the lane's fragment is
+// image row rbase + (i>>2) + rstep*(j>>2) + ... (see tr_frag)
+ORION_DEVICE bf16x8 tr_frag_asm(const bf16_t* img, int rbase, int cbase, int lane, int rstep = 8) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = rbase + (i >> 2);
+  const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
+  return cat8(tr_read(img, loff<128>(row, col)), tr_read(img, loff<128>(row + rstep, col)));
+}
+
+// wait until at most N LDS reads are outstanding; the fragments are "+v" operands so
+// no MFMA reading them can be scheduled before the wait
+template <int N, int TA>
+ORION_DEVICE void lds_wait_frags(bf16x8 (&af)[TA], bf16x8 (&bf)[2]) {
+  if constexpr (TA == 4) {
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bf[0]), "+v"(bf[1])
+                 : "n"(N));
+  } else if constexpr (TA == 2) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(af[0]), "+v"(af[1]), "+v"(bf[0]), "+v"(bf[1]) : "n"(N));
+  } else {
+    static_assert(TA == 1, "TA in {1, 2, 4}");
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(af[0]), "+v"(bf[0]), "+v"(bf[1]) : "n"(N));
+  }
+}
+
+template <int N>
+ORION_DEVICE void wait_vm_exact() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 }  // namespace orion

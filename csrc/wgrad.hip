@@ -24,51 +24,6 @@
 namespace orion {
 
 
-ORION_DEVICE void glds16(const bf16_t* g, bf16_t* l) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
-}
-
-// ds_read_b64_tr_b16 as inline asm: LDS reads the compiler cannot see, so its waitcnt
-// pass does not drain the in-flight LDS-DMA ring (vmcnt(0)) before them (the builtin
-// form gets exactly that).  Completion is waited for by hand (lgkmcnt, below).
-ORION_DEVICE bf16x4 tr_read(const bf16_t* lds, int elem) {
-  const unsigned addr =
-      (unsigned)(uintptr_t)((const __attribute__((address_space(3))) bf16_t*)(lds + elem));
-  bf16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
-}
-
-// tr_frag (mfma_lds.h) on the asm read, [rows][128] image, rows r and r + 8
-ORION_DEVICE bf16x8 tr_frag_asm(const bf16_t* img, int rbase, int cbase, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const int row = rbase + (i >> 2);
-  const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
-  return cat8(tr_read(img, loff<128>(row, col)), tr_read(img, loff<128>(row + 8, col)));
-}
-
-// wait until at most N LDS reads are outstanding; the fragments are "+v" operands so
-// no MFMA reading them can be scheduled before the wait
-template <int N, int TA>
-ORION_DEVICE void lds_wait_frags(bf16x8 (&af)[TA], bf16x8 (&bf)[2]) {
-  if constexpr (TA == 4) {
-    asm volatile("s_waitcnt lgkmcnt(%6)"
-                 : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bf[0]), "+v"(bf[1])
-                 : "n"(N));
-  } else if constexpr (TA == 2) {
-    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(af[0]), "+v"(af[1]), "+v"(bf[0]), "+v"(bf[1]) : "n"(N));
-  } else {
-    static_assert(TA == 1, "TA in {1, 2, 4}");
-    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(af[0]), "+v"(bf[0]), "+v"(bf[1]) : "n"(N));
-  }
-}
-
-template <int N>
-ORION_DEVICE void wait_vm_exact() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 // Staging is LDS-DMA (global_load_lds_dwordx4): no VGPRs, so a ring of NS stages
 // keeps NS-1 stages per CU in flight (register staging held 32-48 KB and ran
 // latency-bound at ~0.8 PF/s).  A wave-instruction writes 1 KB lane-linearly (4

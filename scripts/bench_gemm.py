@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""GEMM microbenchmark on the GPT-2-124M training shapes (M = 64 x 1024 tokens):
+csrc/gemm.hip (with its fused epilogues) vs hipBLASLt through PyTorch (committed TunableOp
+table loaded) plus the separate HIP epilogue kernels it needs.  Interleaved rounds in one
+process, median per variant; one JSON line per shape.
+
+usage: python scripts/bench_gemm.py [--M 65536] [--iters 20] [--check]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fns, iters):
+    """fns: dict name -> callable; interleaved rounds, median ms per name."""
+    for f in fns.values():
+        for _ in range(3):
+            f()
+    torch.cuda.synchronize()
+    ts = {k: [] for k in fns}
+    for _ in range(iters):
+        for k, f in fns.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            f()
+            b.record()
+            b.synchronize()
+            ts[k].append(a.elapsed_time(b))
+    return {k: sorted(v)[len(v) // 2] for k, v in ts.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--check", action="store_true", help="compare outputs against torch")
+    a = ap.parse_args()
+    from orion_amd.ops._ext import C, load_ext
+    from orion_amd.tuning import use_tuned_gemms
+    load_ext(required=True)
+    use_tuned_gemms()
+    ops = C()
+    M = a.M
+    g = torch.Generator(device="cuda").manual_seed(0)
+    rnd = lambda *s: (torch.randn(*s, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    # (name, kind, N, K, epi): fwd = x (M,K) . W(N,K)^T; dgrad = dy (M,K) . W(K,N)
+    shapes = [("qkv_fwd", "fwd", 2304, 768, 1), ("attnproj_fwd", "fwd", 768, 768, 0),
+              ("fc_fwd+bias+gelu", "fwd", 3072, 768, 2), ("mlpproj_fwd", "fwd", 768, 3072, 0),
+              ("lmhead_fwd", "fwd", 50304, 768, 0),
+              ("qkv_dgrad", "dgrad", 768, 2304, 0), ("attnproj_dgrad", "dgrad", 768, 768, 0),
+              ("fc_dgrad", "dgrad", 768, 3072, 0), ("mlpproj_dgrad+gelu_bwd", "dgrad", 3072, 768, 3),
+              ("lmhead_dgrad", "dgrad", 768, 50304, 0)]
+    tot = {"hip": 0.0, "blas": 0.0}
+    for name, kind, N, K, epi in shapes:
+        x = rnd(M, K)
+        w = rnd(N, K) if kind == "fwd" else rnd(K, N)
+        b = rnd(N) if epi in (1, 2) else None
+        pre = rnd(M, N) if epi == 3 else None
+        if kind == "fwd":
+            hip = lambda: ops.gemm(x, w, False, epi, b, None)
+            if epi == 2:
+                blas = lambda: ops.bias_gelu_fwd(torch.nn.functional.linear(x, w), b)
+            else:
+                blas = lambda: torch.nn.functional.linear(x, w, b)
+        else:
+            hip = lambda: ops.gemm(x, w, True, epi, None, pre)
+            if epi == 3:
+                # the unfused path: dgrad GEMM, then the GELU backward kernel (x = pre, no bias)
+                blas = lambda: ops.bias_gelu_bwd(x @ w, pre, None, None)
+            else:
+                blas = lambda: x @ w
+        t = timeit({"hip": hip, "blas": blas}, a.iters)
+        flop = 2.0 * M * N * K
+        rec = {"shape": name, "M": M, "N": N, "K": K, "epi": epi,
+               "hip_ms": round(t["hip"], 4), "blas_ms": round(t["blas"], 4),
+               "hip_TFs": round(flop / t["hip"] / 1e9, 1), "blas_TFs": round(flop / t["blas"] / 1e9, 1)}
+        if a.check:
+            ref = (x.float() @ (w.float().t() if kind == "fwd" else w.float()))
+            if b is not None:
+                ref = ref + b.float()
+            got = hip()
+            o = got[0].float()
+            if epi == 3:
+                from orion_amd.ops import reference as R
+                gp = torch.func.grad(lambda z: R.gelu_tanh(z).sum())
+                ref = ref * gp(pre.float())
+            rec["rel_err"] = float((o - ref).norm() / ref.norm())
+            if epi == 2:
+                from orion_amd.ops import reference as R
+                rec["rel_err_gelu"] = float((got[1].float() - R.gelu_tanh(ref)).norm() / R.gelu_tanh(ref).norm())
+        tot["hip"] += t["hip"]
+        tot["blas"] += t["blas"]
+        print(json.dumps(rec), flush=True)
+        del x, w, b, pre
+    print(json.dumps({"total_hip_ms": round(tot["hip"], 3), "total_blas_ms": round(tot["blas"], 3)}))
+
+
+if __name__ == "__main__":
+    main()

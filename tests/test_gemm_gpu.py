@@ -1,0 +1,79 @@
+"""csrc/gemm.hip (forward NT / input-gradient NN GEMMs with fused epilogues) against an fp32
+PyTorch reference, including ragged M and N (partial 256 x 256 tiles) and the epilogues
+(bias, bias + GELU with the pre-activation output, GELU backward)."""
+import pytest
+import torch
+
+from orion_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _C():
+    from orion_amd.ops._ext import C, load_ext
+    load_ext(required=True)
+    return C()
+
+
+def _rnd(g, *s):
+    return (torch.randn(*s, device=DEV, generator=g) * 0.5).to(torch.bfloat16)
+
+
+def _gelu_grad(z):
+    return torch.func.vmap(torch.func.grad(lambda t: ref.gelu_tanh(t)))(z.reshape(-1)).view_as(z)
+
+
+SHAPES = [(256, 256, 64), (300, 264, 128), (1000, 768, 768), (513, 1000, 192), (64, 8, 64),
+          (4096, 2304, 768), (2048, 3072, 768), (1024, 768, 3072), (777, 50304, 128)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("wkm", [False, True])
+def test_gemm_store(M, N, K, wkm):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    x = _rnd(g, M, K)
+    w = _rnd(g, K, N) if wkm else _rnd(g, N, K)
+    out, _ = _C().gemm(x, w, wkm, 0, None, None)
+    want = x.float() @ (w.float() if wkm else w.float().t())
+    assert out.shape == (M, N)
+    assert rel_err(out, want) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES[:6])
+def test_gemm_bias_and_bias_gelu(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(7 + M)
+    x, w, b = _rnd(g, M, K), _rnd(g, N, K), _rnd(g, N)
+    a = x.float() @ w.float().t() + b.float()
+    out, none = _C().gemm(x, w, False, 1, b, None)
+    assert rel_err(out, a) < 1e-2
+    pre, h = _C().gemm(x, w, False, 2, b, None)
+    assert rel_err(pre, a) < 1e-2
+    assert rel_err(h, ref.gelu_tanh(a)) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES[:6])
+def test_gemm_gelu_backward_epilogue(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(11 + N)
+    dy, w, pre = _rnd(g, M, K), _rnd(g, K, N), _rnd(g, M, N)
+    out, _ = _C().gemm(dy, w, True, 3, None, pre)
+    want = (dy.float() @ w.float()) * _gelu_grad(pre.float())
+    assert rel_err(out, want) < 1e-2
+
+
+def test_gemm_batched_input_shape_and_strided_rows():
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = _rnd(g, 4, 96, 256)
+    w = _rnd(g, 512, 256)
+    out, _ = _C().gemm(x, w, False, 0, None, None)
+    assert out.shape == (4, 96, 512)
+    assert rel_err(out, x.float() @ w.float().t()) < 1e-2
+    big = _rnd(g, 300, 2304)           # a column slice of a wider buffer (row stride 2304)
+    xs = big[:, 768:1536]
+    out2, _ = _C().gemm(xs, w[:, :256].contiguous().repeat(1, 3), False, 0, None, None)
+    assert rel_err(out2, xs.float() @ w[:, :256].float().repeat(1, 3).t()) < 1e-2
