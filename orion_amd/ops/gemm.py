@@ -65,12 +65,11 @@ def wgrad_into(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate:
     n1, n2 = dy.shape[1], x.shape[1]
     if scale is None and _blas_wins(n1, n2):
         o2 = out.view(n1, n2)
-        if o2.dtype == torch.float32:  # fp32 gradient arena: hipBLASLt with fp32 output
-            g = torch.mm(dy.t(), x, out_dtype=torch.float32)
+        if o2.dtype == torch.float32:  # fp32 gradient arena: hipBLASLt with fp32 output, in place
             if accumulate:
-                o2.add_(g)
+                torch.addmm(o2, dy.t(), x, out_dtype=torch.float32, out=o2)
             else:
-                o2.copy_(g)
+                torch.mm(dy.t(), x, out_dtype=torch.float32, out=o2)
         elif accumulate:
             torch.addmm(o2, dy.t(), x, out=o2)
         else:

@@ -121,6 +121,7 @@ class Trainer:
             _, loss = self.model(x, y)
             (loss / n).backward()
             losses.append(loss.detach())
+        self.arena.finish_grads()
         if self.reducer is not None:
             self.reducer.finish()
         self.opt.step()
@@ -136,6 +137,7 @@ class Trainer:
             _, loss = self.model(x, y)
             (loss / n).backward()
             losses.append(loss.detach())
+        self.arena.finish_grads()
         self.opt.step(hyper_prefilled=True)
         return torch.stack(losses).mean()
 
