@@ -290,6 +290,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
     for (int i = 0; i < NST; ++i) {
       const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
       const long key = min(t * BN + row, p.Tk - 1);
+      ORION_DASSERT(key >= 0 && ch * 8 + 8 <= D);
       kst[i] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ch * 8);
       vst[i] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ch * 8);
     }
@@ -358,6 +359,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   }
 
   if (myq < p.T) {
+    ORION_DASSERT(b < p.B && hq < p.Hq);
     bf16_t* Qo = p.dq + b * p.dq_sb + hq * p.dq_sh + (long)myq * p.dq_st;
 #pragma unroll
     for (int db = 0; db < NDB; ++db)

@@ -14,6 +14,15 @@
 
 #define ORION_DEVICE __device__ __forceinline__
 
+// Device-side bounds checks, compiled in only by the debug build (ORION_AMD_DEBUG=1,
+// orion_amd/build.py): a failing check prints the kernel, line and condition and traps.
+#ifdef ORION_DEBUG
+#include <assert.h>
+#define ORION_DASSERT(cond) assert(cond)
+#else
+#define ORION_DASSERT(cond) ((void)0)
+#endif
+
 namespace orion {
 
 typedef unsigned short bf16_t;  // raw bf16 bits

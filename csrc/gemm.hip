@@ -66,6 +66,7 @@ ORION_DEVICE void gemm_epilogue_tile(const GemmArgs& g, const f32x16& acc, int m
       for (int e = 0; e < 4; ++e) v[e] += bf2f(b4[e]);
     }
     if constexpr (EPI == EPI_GELU_BWD) {
+      ORION_DASSERT(mc < g.M && nc + 4 <= g.N);
       const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(g.pre + (long)mc * g.ldp + nc);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] *= gelu_tanh_grad_f(bf2f(a4[e]));
@@ -89,6 +90,7 @@ ORION_DEVICE void gemm_epilogue_tile(const GemmArgs& g, const f32x16& acc, int m
       a0 = r0[0]; b0 = r0[1]; a1 = r1[0]; b1 = r1[1];
       const int n = nb + 16 * pr + 8 * h32;
       if (m < g.M && n < g.N) {
+        ORION_DASSERT(n + 8 <= g.N && m >= 0);
         uint4 w;
         w.x = a0; w.y = a1; w.z = b0; w.w = b1;
         *reinterpret_cast<uint4*>(base + (long)m * ld + n) = w;
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(GemmArgs g) {
     }
   }
   auto issue_x = [&](int t, int i) {
+    ORION_DASSERT((t + 1) * BK <= g.K && gx[i] / g.ldx < g.M);
     glds16(g.X + (long)t * BK + gx[i], smem + (t % NS) * STAGE + lx[i]);
   };
   auto issue_w = [&](int t, int i) {

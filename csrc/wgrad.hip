@@ -78,6 +78,7 @@ __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
     const long mr = m0 + (long)step * BK;
 #pragma unroll
     for (int i = 0; i < BPW; ++i) {
+      ORION_DASSERT(mr + BK <= M && goffA[i] % lda + 8 <= N1 && goffB[i] % ldb + 8 <= N2);
       glds16(A + mr * lda + goffA[i], base + loffs[i]);
       glds16(B + mr * ldb + goffB[i], base + 2 * IMG + loffs[i]);
     }
@@ -158,6 +159,7 @@ __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
       for (int r = 0; r < 16; ++r) {
         const int n1 = n10 + wr * TA * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
         if (n1 < N1 && n2 < N2) {
+          ORION_DASSERT(n1 >= 0 && n2 >= 0);
           if (sl) sl[(long)n1 * N2 + n2] = acc[a][b][r];
           else {
             const long o = (long)n1 * N2 + n2;

@@ -22,8 +22,13 @@ import sysconfig
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.environ.get("ORION_AMD_CSRC", os.path.join(ROOT, "csrc"))
-BUILD = os.environ.get("ORION_AMD_BUILD_DIR", os.path.join(ROOT, "build", "csrc"))
-OUT = os.environ.get("ORION_AMD_EXT", os.path.join(ROOT, "orion_amd", "_C.so"))
+# ORION_AMD_DEBUG=1: -O1 -g with device-side bounds asserts on the global indices of the
+# hand-written kernels (ORION_DASSERT in csrc/common.h), built beside the release library
+# as orion_amd/_C_debug.so; load it with ORION_AMD_EXT=orion_amd/_C_debug.so.
+DEBUG = os.environ.get("ORION_AMD_DEBUG") == "1"
+_SUFFIX = "_debug" if DEBUG else ""
+BUILD = os.environ.get("ORION_AMD_BUILD_DIR", os.path.join(ROOT, "build", "csrc" + _SUFFIX))
+OUT = os.environ.get("ORION_AMD_EXT", os.path.join(ROOT, "orion_amd", f"_C{_SUFFIX}.so"))
 ARCH = os.environ.get("ORION_AMD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
@@ -54,7 +59,8 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     incs, libdirs, abi = _torch_paths()
     os.makedirs(BUILD, exist_ok=True)
     hdr_time = _newest_header()
-    common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+    opt = ["-O1", "-g", "-DORION_DEBUG=1"] if DEBUG else ["-O3"]
+    common = [*opt, "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
               "-Wno-unused-result", "-Wno-unused-command-line-argument", f"-I{CSRC}"]
     kern = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
             *common]

@@ -20,11 +20,59 @@ scalar (the LM head's loss scale).  Measured on MI355X at M = 65,536:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
 
 from ._ext import C
+
+# ------------------------------------------------------------------ forward / dgrad GEMMs
+# Linear-layer forward (x W^T [+ b]) and input gradient (dy W) run on hipBLASLt by default
+# (csrc/gemm.hip measures 0.75-1.05 PF/s against hipBLASLt's 0.9-1.4 on the GPT-2 shapes:
+# docs/PERFORMANCE.md).  The in-tree kernel is used when ORION_GEMM=hip, and always inside
+# a HIP-graph capture (``hip_gemms()``): its arguments are plain kernel arguments captured
+# in the graph node, with no library-side host state between replays.
+_GEMM_IMPL = os.environ.get("ORION_GEMM", "blas")  # "blas" | "hip"
+_FORCE_HIP = 0
+
+EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD = 0, 1, 2, 3
+
+
+@contextlib.contextmanager
+def hip_gemms():
+    """Route eligible linear-layer GEMMs to csrc/gemm.hip inside the block."""
+    global _FORCE_HIP
+    _FORCE_HIP += 1
+    try:
+        yield
+    finally:
+        _FORCE_HIP -= 1
+
+
+def use_hip_gemm(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
+    if not (_FORCE_HIP or _GEMM_IMPL == "hip"):
+        return False
+    K = x.shape[-1]
+    N = w.shape[1] if w_kmajor else w.shape[0]
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and K % 64 == 0 and N % 8 == 0 and w.is_contiguous() and x.stride(-1) == 1
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and (x.dim() == 2 and x.stride(0) % 8 == 0 or x.is_contiguous()))
+
+
+def linear_fwd(x, w, b=None):
+    """x W^T (+ b): csrc/gemm.hip when selected (see above), else hipBLASLt."""
+    if use_hip_gemm(x, w, False):
+        return C().gemm(x, w, False, EPI_BIAS if b is not None else EPI_STORE, b, None)[0]
+    return torch.nn.functional.linear(x, w, b)
+
+
+def linear_dgrad(dy, w):
+    """dy W for W (N_out, N_in): the input gradient of x W^T."""
+    if use_hip_gemm(dy, w, True):
+        return C().gemm(dy, w, True, EPI_STORE, None, None)[0]
+    return dy @ w
 
 _FORCE = os.environ.get("ORION_WGRAD_SPLITS")
 _IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/wgrad.hip) | "bmm"

@@ -6,7 +6,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
-from .gemm import wgrad, wgrad_into
+from .gemm import linear_dgrad, linear_fwd, wgrad, wgrad_into
 from .grad_sink import claim, sink_of
 
 
@@ -108,8 +108,9 @@ def add_layer_norm_hip(x, r, weight, bias, eps=1e-5, r_bias=None):
 
 
 class _Linear(torch.autograd.Function):
-    """y = x W^T + b on hipBLASLt; backward computes the bias gradient with the
-    deterministic two-stage column-sum kernel instead of a generic reduction."""
+    """y = x W^T + b on hipBLASLt (or csrc/gemm.hip: ops/gemm.py); backward computes the
+    bias gradient with the deterministic two-stage column-sum kernel instead of a generic
+    reduction."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -117,7 +118,7 @@ class _Linear(torch.autograd.Function):
         ctx.has_bias = b is not None
         ctx.sink = sink_of(w)  # dW straight into the gradient arena (ops/grad_sink.py)
         ctx.bias = b
-        return torch.nn.functional.linear(x, w, b)
+        return linear_fwd(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
@@ -125,7 +126,7 @@ class _Linear(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = (dy2 @ w).view(x.shape)
+            dx = linear_dgrad(dy2, w).view(x.shape)
         if ctx.needs_input_grad[1]:
             sink = ctx.sink
             if sink is not None:

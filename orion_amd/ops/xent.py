@@ -10,14 +10,14 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
-from .gemm import wgrad, wgrad_into
+from .gemm import linear_dgrad, linear_fwd, wgrad, wgrad_into
 from .grad_sink import sink_of
 
 
 class _LinearXent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, targets, ignore_index):
-        logits = torch.nn.functional.linear(x, w)
+        logits = linear_fwd(x, w)
         loss = C().xent_fwd_bwd(logits, targets.contiguous(), int(ignore_index))
         ctx.save_for_backward(x, w, logits)   # logits now hold dlogits / n_valid
         ctx.sink = sink_of(w)
@@ -29,7 +29,7 @@ class _LinearXent(torch.autograd.Function):
         s = g.detach().float().reshape(1).contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = dl @ w
+            dx = linear_dgrad(dl, w)
             C().scale_(dx, s)
         if ctx.needs_input_grad[1]:
             sink = ctx.sink

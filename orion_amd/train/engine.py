@@ -16,6 +16,7 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+from ..ops.gemm import hip_gemms
 from .flat import FlatArena
 from .optim import FlatAdamW
 
@@ -58,13 +59,13 @@ class Trainer:
     what bounds small models and small micro-batches."""
 
     GRAPH_WARMUP = 2
-    # Captured steps are validated against eager (same loss trajectory) up to 8192 tokens
-    # per micro-batch.  At 65,536 tokens the third replay of the 12-layer GPT-2 step hits
-    # a memory-aperture violation inside the library GEMMs (our kernels have no host-side
-    # state in the graph since the dQ zeroing moved out of hipMemsetAsync), and routing the
-    # capture through rocBLAS gave NaNs even at small shapes -- so larger micro-batches run
-    # eagerly, where launch overhead is < 0.2 % of the step anyway.
-    GRAPH_MAX_TOKENS = int(os.environ.get("ORION_GRAPH_MAX_TOKENS", 8192))
+    # The warm-up and the capture run every linear-layer GEMM on csrc/gemm.hip
+    # (ops.gemm.hip_gemms): in round 1 the captured hipBLASLt GEMMs faulted (memory-aperture
+    # violation) on the third replay at 65,536 tokens per micro-batch and rocBLAS gave NaNs,
+    # which is why capture used to be capped at 8,192 tokens.  With the in-tree GEMM every
+    # kernel of the step takes its arguments by value, so a replay depends on no host-side
+    # library state.  ORION_GRAPH_MAX_TOKENS still caps the captured micro-batch (0 = none).
+    GRAPH_MAX_TOKENS = int(os.environ.get("ORION_GRAPH_MAX_TOKENS", 0))
 
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float = 64.0, arena_dtype=None,
@@ -102,7 +103,8 @@ class Trainer:
 
     def step(self, batches):
         """batches: sequence of (idx, targets) micro-batches.  Returns mean loss (device)."""
-        if self.graph_enabled and self._graph is None and batches[0][0].numel() > self.GRAPH_MAX_TOKENS:
+        if (self.graph_enabled and self._graph is None and self.GRAPH_MAX_TOKENS
+                and batches[0][0].numel() > self.GRAPH_MAX_TOKENS):
             print(f"[orion_amd] HIP-graph capture is validated up to {self.GRAPH_MAX_TOKENS} tokens "
                   f"per micro-batch; running {batches[0][0].numel()} eagerly", flush=True)
             self.graph_enabled = False
@@ -149,7 +151,7 @@ class Trainer:
             if self._side is None:
                 self._side = torch.cuda.Stream()
             self._side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self._side):
+            with torch.cuda.stream(self._side), hip_gemms():
                 self.opt.hyper_tensor()
                 loss = self._body(batches)
             torch.cuda.current_stream().wait_stream(self._side)
@@ -160,7 +162,7 @@ class Trainer:
             self.opt.hyper_tensor()
             self._graph = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
-            with torch.cuda.graph(self._graph):
+            with torch.cuda.graph(self._graph), hip_gemms():
                 self._static_loss = self._body(self._static)
             self.opt.step_count -= 1  # the capture ran nothing; the replay below is the step
         else:

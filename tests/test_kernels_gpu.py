@@ -409,10 +409,12 @@ def test_xent_ignore_index_and_unaligned_targets():
     assert rel_err(x.grad, xr.grad) < 2e-2 and rel_err(w.grad, wr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("shape", [("gpt2-tiny", 4, 64, 2, {}), ("gpt2", 8, 1024, 1, dict(n_layer=2))])
+@pytest.mark.parametrize("shape", [("gpt2-tiny", 4, 64, 2, {}), ("gpt2", 8, 1024, 1, dict(n_layer=2)),
+                                   ("gpt2", 64, 1024, 1, {})])
 def test_trainer_hip_graph_matches_eager(shape):
     """the graph-captured step (warm-up, capture, replays) follows the eager trajectory;
-    the GPT-2-width case exercises the split-K wgrad slabs and the attention atomics."""
+    the GPT-2-width case exercises the split-K wgrad slabs; the last case is the full
+    12-layer GPT-2 at the bench micro-batch (65,536 tokens), which round 1 had to cap."""
     from orion_amd.models.gpt2 import build_gpt2
     from orion_amd.train.engine import Trainer, OptimConfig
     name, B, T, A, over = shape
@@ -584,3 +586,27 @@ def test_zero_grad_skips_sink_slices_and_finish_zeroes_unwritten():
         loss.backward()
         arena.finish_grads()
     assert rel_err(a.grads, a2.grads) < 1e-2
+
+
+def test_in_tree_gemm_path_matches_hipblaslt_in_the_model():
+    """GPT-2 (2 layers) forward + backward with every linear-layer GEMM on csrc/gemm.hip
+    (ops.gemm.hip_gemms: the HIP-graph capture path) vs the hipBLASLt path."""
+    from orion_amd.models.gpt2 import build_gpt2
+    from orion_amd.ops.gemm import hip_gemms
+    torch.manual_seed(0)
+    m = build_gpt2("gpt2", n_layer=2, block_size=256).to(DEV).to(torch.bfloat16)
+    x = torch.randint(0, 50257, (4, 256), device=DEV)
+    res = []
+    for use in (False, True):
+        m.zero_grad(set_to_none=True)
+        if use:
+            with hip_gemms():
+                _, loss = m(x, x)
+                loss.backward()
+        else:
+            _, loss = m(x, x)
+            loss.backward()
+        res.append((float(loss), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    assert abs(res[0][0] - res[1][0]) < 1e-2
+    for n in res[0][1]:
+        assert rel_err(res[1][1][n], res[0][1][n]) < 2e-2, n
