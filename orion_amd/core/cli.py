@@ -65,9 +65,9 @@ def main(argv=None):
               max_broken=execution.get("max_broken", 3))
     n = int(execution.get("workers", 1) or 1)
     if n > 1:
-        workon_pool(_Rebuild(exp.name, db_opts, exp.metadata["user"]), n, **kw)
-    else:
-        workon(exp, **kw)
+        # a crashed worker process makes the CLI fail instead of reporting success
+        return 1 if workon_pool(_Rebuild(exp.name, db_opts, exp.metadata["user"]), n, **kw) else 0
+    workon(exp, **kw)
     return 0
 
 

@@ -215,6 +215,8 @@ def merge_orion_config(config, dbconfig, cmdconfig, cmdargs):
     exp = deepcopy(config)
     for cfg in (dbconfig, cmdconfig):
         for k, v in (cfg or {}).items():
+            if v is None:  # unset (a new experiment's attributes): keep the layer below
+                continue
             if k in ENV_VARS and isinstance(v, dict):
                 for vk, vv in v.items():
                     exp[k][vk] = vv

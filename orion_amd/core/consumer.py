@@ -150,6 +150,10 @@ class Consumer:
         while True:
             lease = self.gpu_pool.try_acquire(self.gpus_per_trial)
             if lease is not None:
+                if not self.experiment.record_lease(trial, lease.ids):
+                    lease.release()
+                    raise TrialLost(trial.id)
+                self._last_beat = time.monotonic()
                 return lease
             self._beat(trial)
             time.sleep(min(poll, self.heartbeat))

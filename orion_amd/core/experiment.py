@@ -189,6 +189,18 @@ class Experiment:
             upd["end_time"] = trial.end_time = utcnow()
         return self._db.read_and_write("trials", q, upd) is not None
 
+    def record_lease(self, trial, gpu_ids):
+        """The trial got its GPUs and starts executing: record the device ids and move
+        ``start_time`` from the reservation to now (a reserved trial may wait for a GPU
+        lease first).  False if the trial is no longer ours."""
+        now = utcnow()
+        ok = self._db.read_and_write("trials", {"_id": trial.id, "status": "reserved"},
+                                     {"gpus": list(gpu_ids), "start_time": now,
+                                      "heartbeat": now}) is not None
+        if ok:
+            trial.gpus, trial.start_time = list(gpu_ids), now
+        return ok
+
     def update_heartbeat(self, trial):
         return self._db.read_and_write("trials", {"_id": trial.id, "status": "reserved"},
                                        {"heartbeat": utcnow()}) is not None

@@ -84,4 +84,6 @@ def workon_pool(experiment_factory, n_workers, **kwargs):
     for p in procs:
         p.join()
         code = code or p.exitcode
+    if code:
+        log.error("a worker process exited with status %s", code)
     return code

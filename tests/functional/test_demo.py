@@ -116,3 +116,26 @@ def test_orion_tunes_train_py(tmp_path):
         assert p["name"] == "/learning_rate" and 1e-4 <= p["value"] < 1e-2
         (r,) = [r for r in t["results"] if r["type"] == "objective"]
         assert r["name"] == "val_loss" and r["value"] > 0
+
+
+def test_cli_workers_flag_with_default_pool_size(tmp_path):
+    """``--workers 2`` starts two worker processes that rebuild the experiment from the
+    store; with no --pool-size the stored document must carry the default pool size (a
+    new experiment's unset attributes must not override the defaults), and a GPU lease
+    (--gpus-per-trial 1 on one device id) serialises the trials."""
+    db = str(tmp_path / "orion.sqlite")
+    env = _env(db)
+    env.update(ORION_GPUS="0", TMPDIR=str(tmp_path))
+    rc = subprocess.call(ORION + ["-n", "workers_flag", "--max-trials", "6", "--workers", "2",
+                                  "--gpus-per-trial", "1", "./black_box.py", "-x~uniform(-50, 50)"],
+                         cwd=DEMO, env=env, timeout=600)
+    assert rc == 0
+    store = Database("sqlite", host=db)
+    (exp,) = store.read("experiments", {"name": "workers_flag"})
+    assert exp["pool_size"] == 10 and exp["status"] == "done"
+    trials = store.read("trials", {"experiment": exp["_id"]})
+    done = [t for t in trials if t["status"] == "completed"]
+    assert len(done) >= 6
+    assert all(t["gpus"] == ["0"] for t in done)
+    spans = sorted((t["start_time"], t["end_time"]) for t in done)
+    assert all(b[0] >= a[1] for a, b in zip(spans, spans[1:])), "GPU lease held twice"
