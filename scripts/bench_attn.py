@@ -73,7 +73,8 @@ def main():
     if Hkv != H:
         kt, vt = (t.detach().repeat_interleave(H // Hkv, 1).requires_grad_() for t in (kt, vt))
     try:
-        res["sdpa_fwd_ms"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qt, kt, vt, is_causal=causal))
+        sdpa = torch.nn.functional.scaled_dot_product_attention
+        res["sdpa_fwd_ms"] = timeit(lambda: sdpa(qt, kt, vt, is_causal=causal))
         out = torch.nn.functional.scaled_dot_product_attention(qt, kt, vt, is_causal=causal)
         g = torch.randn_like(out)
         res["sdpa_bwd_ms"] = timeit(lambda: torch.autograd.grad(out, (qt, kt, vt), g, retain_graph=True))

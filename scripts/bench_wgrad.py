@@ -39,7 +39,8 @@ def main():
             except Exception as e:  # pragma: no cover
                 r[f"split{S}"] = str(e)[:80]
         ref = (dy.float().t() @ x.float())
-        err = ((torch.bmm(dy.view(8, -1, n1).transpose(1, 2), x.view(8, -1, n2), out_dtype=torch.float32).sum(0) - ref).abs().max() / ref.abs().max()).item()
+        got = torch.bmm(dy.view(8, -1, n1).transpose(1, 2), x.view(8, -1, n2), out_dtype=torch.float32).sum(0)
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
         out[f"{n1}x{n2}"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
         out[f"{n1}x{n2}"]["best_PFs"] = round(fl / min(v for v in r.values() if isinstance(v, float)) / 1e12, 3)
         out[f"{n1}x{n2}"]["split8_relerr"] = err

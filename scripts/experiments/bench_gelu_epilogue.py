@@ -60,7 +60,7 @@ def rel(a, b):
 
 
 # numerics
-import os, sys
+import sys
 try:
     a2, h2 = fwd_epi()
 except RuntimeError as e:
@@ -89,4 +89,5 @@ tb, te = timeit(fwd_base), (timeit(fwd_epi) if fwd_epi else float("nan"))
 print(f"fwd ms: base {tb:.3f}  epilogue {te:.3f}", flush=True)
 tb, te = timeit(bwd_base), timeit(bwd_epi)
 print(f"bwd ms: base {tb:.3f}  epilogue {te:.3f}", flush=True)
-print(f"plain F.linear fwd ms {timeit(lambda: F.linear(x, wfc)):.3f}  dy@wpr ms {timeit(lambda: dy @ wpr):.3f}", flush=True)
+t_lin, t_dg = timeit(lambda: F.linear(x, wfc)), timeit(lambda: dy @ wpr)
+print(f"plain F.linear fwd ms {t_lin:.3f}  dy@wpr ms {t_dg:.3f}", flush=True)

@@ -52,7 +52,8 @@ def main():
     cats = {}
     for n, (c, t) in agg.items():
         cats[category(n)] = cats.get(category(n), 0.0) + t
-    print("\nby category (ms/step):", ", ".join(f"{k}={v / a.steps:.2f}" for k, v in sorted(cats.items(), key=lambda kv: -kv[1])))
+    ranked = sorted(cats.items(), key=lambda kv: -kv[1])
+    print("\nby category (ms/step):", ", ".join(f"{k}={v / a.steps:.2f}" for k, v in ranked))
 
 
 if __name__ == "__main__":

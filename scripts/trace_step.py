@@ -24,5 +24,6 @@ for r in seq:
 tot = sum(v[1] for v in agg.values())
 span = (int(seq[-1]["End_Timestamp"]) - int(seq[0]["Start_Timestamp"])) / 1e3
 print(f"step kernels: {len(seq)}  busy {tot / 1e3:.2f} ms  span {span / 1e3:.2f} ms")
-for (n, gx, gy, gz, wg), (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:int(sys.argv[2]) if len(sys.argv) > 2 else 40]:
+top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+for (n, gx, gy, gz, wg), (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
     print(f"{n:60s} grid=({gx},{gy},{gz}) wg={wg:4s} x{c:3d}  {t / 1e3:7.3f} ms  {t / c:8.1f} us/call")

@@ -4,12 +4,11 @@ core/test_trial.py, core/test_utils_format.py, client/test_client.py,
 core/convert_test.py)."""
 import importlib
 import json
-import os
 
 import numpy as np
 import pytest
 
-from orion_amd.algo import BaseAlgorithm, OptimizationAlgorithm, register_algorithm
+from orion_amd.algo import BaseAlgorithm, OptimizationAlgorithm
 from orion_amd.core import config as rc
 from orion_amd.core.format_trials import get_trial_results, trial_to_tuple, tuple_to_trial
 from orion_amd.core.primary_algo import PrimaryAlgo

@@ -2,7 +2,6 @@
 keeps heart-beating, and a trial re-queued by another worker's reaper is abandoned --
 never run a second time or completed twice."""
 import os
-import sys
 import textwrap
 import threading
 import time

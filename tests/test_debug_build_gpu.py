@@ -32,7 +32,8 @@ print("debug build ok")
 """
 
 
-@pytest.mark.skipif(not os.path.isfile(DEBUG_SO), reason="debug build not present (ORION_AMD_DEBUG=1 python -m orion_amd.build)")
+@pytest.mark.skipif(not os.path.isfile(DEBUG_SO),
+                    reason="debug build not present (ORION_AMD_DEBUG=1 python -m orion_amd.build)")
 def test_debug_build_kernels_pass_their_bounds_asserts():
     env = dict(os.environ, ORION_AMD_EXT=DEBUG_SO, PYTHONPATH=ROOT)
     out = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True,

@@ -1,6 +1,5 @@
 """Prior DSL and templating (reference: tests/unittests/core/test_space_builder.py)."""
 import json
-import os
 
 import numpy as np
 import pytest
@@ -70,8 +69,12 @@ class TestDimensionBuilder:
 
 @pytest.fixture
 def yaml_tmpl(tmp_path):
-    data = {"yo": 5, "training": {"lr0": "orion~loguniform(0.0001, 0.3)", "mbs": "orion~uniform(32, 256, discrete=True)"},
-            "layers": [{"width": 64, "type": "relu"}, {"width": "orion~uniform(32, 256, discrete=True)", "type": "orion~choices(['relu', 'sigmoid'])"}]}
+    data = {"yo": 5,
+            "training": {"lr0": "orion~loguniform(0.0001, 0.3)",
+                         "mbs": "orion~uniform(32, 256, discrete=True)"},
+            "layers": [{"width": 64, "type": "relu"},
+                       {"width": "orion~uniform(32, 256, discrete=True)",
+                        "type": "orion~choices(['relu', 'sigmoid'])"}]}
     p = tmp_path / "cfg.yaml"
     p.write_text(yaml.safe_dump(data))
     return str(p)
@@ -91,7 +94,8 @@ class TestSpaceBuilder:
         s = sb.build_from([f"--config={yaml_tmpl}", "--seed~choices([1, 2])"])
         assert set(s.keys()) == {"/seed", "/training/lr0", "/training/mbs", "/layers/1/width", "/layers/1/type"}
         params = [dict(name=n, type=s[n].type, value=v) for n, v in
-                  (("/layers/1/type", "relu"), ("/layers/1/width", 100), ("/seed", 2), ("/training/lr0", 0.01), ("/training/mbs", 64))]
+                  (("/layers/1/type", "relu"), ("/layers/1/width", 100), ("/seed", 2),
+                   ("/training/lr0", 0.01), ("/training/mbs", 64))]
         out = str(tmp_path / "inst.yaml")
         args = sb.build_to(out, Trial(params=params))
         assert args[0] == "--config=" + out and "--seed=2" in args

@@ -70,7 +70,9 @@ def test_creation_race_duplicate_key(storage):
 def test_create_experiment_retries_race(storage):
     a = Experiment("race2", storage, user="u")
     a.configure(_config(a))
-    exp = create_experiment("race2", storage, dict(cmdargs={"metadata": {"user_args": ["-x~uniform(-50, 50)"], "user_script": "/bin/true"}, "max_trials": 10, "pool_size": 2}), user="u")
+    cmdargs = {"metadata": {"user_args": ["-x~uniform(-50, 50)"], "user_script": "/bin/true"},
+               "max_trials": 10, "pool_size": 2}
+    exp = create_experiment("race2", storage, dict(cmdargs=cmdargs), user="u")
     assert exp.id == a.id
 
 

@@ -3,7 +3,6 @@
 All tests need an MI355X (marker ``gpu``); each one also asserts that the op ran
 through the in-tree extension (``orion_amd/_C.so``), never a silent fallback.
 """
-import math
 
 import pytest
 import torch

@@ -3,7 +3,6 @@ tests/native/host_logic.cpp links the csrc/*.hip launchers compiled host-only wi
 ``-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined`` and exercises split
 planning, scratch sizing and argument rejection.  No GPU: nothing is launched."""
 import os
-import shutil
 import subprocess
 
 import pytest

@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import ast
 import json
-import math
 import os
 import sys
 import time
