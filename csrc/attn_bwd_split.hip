@@ -117,9 +117,10 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 
   bf16x8 qdst[NSTQ];
   float lse_r = 0.f, del_r = 0.f;
-  auto gload = [&](int it) {
-    const int hq = hk * rep + it / iters_per_head;
-    const int qbase = (qi0 + it % iters_per_head) * BMQ;
+  // (head, query tile) of a loop step, walked incrementally (no integer division per tile)
+  auto gload = [&](int h, int qi) {
+    const int hq = hk * rep + h;
+    const int qbase = qi * BMQ;
     const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
     const bf16_t* Db = p.dout + b * p.do_sb + hq * p.do_sh;
     if constexpr (NSTQ >= 2) {
@@ -161,15 +162,25 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
     }
   };
 
+  int nh = 0, nq = qi0;  // next tile to load
+  auto advance = [&](int& h, int& qi) {
+    if (++qi == nqi) { qi = qi0; ++h; }
+  };
   if (total > 0) {
-    gload(0);
+    gload(nh, nq);
+    advance(nh, nq);
     swrite(0);
   }
   __syncthreads();
+  int cq = qi0;  // query tile of this step
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
-    const int qbase = (qi0 + it % iters_per_head) * BMQ;
-    if (it + 1 < total) gload(it + 1);
+    const int qbase = cq * BMQ;
+    if (++cq == nqi) cq = qi0;
+    if (it + 1 < total) {
+      gload(nh, nq);
+      advance(nh, nq);
+    }
     const bf16_t* Qc = Qs + buf * QT;
     const bf16_t* Dc = Ds + buf * QT;
     // wave-uniform: this wave's keys are all above every query of the tile
