@@ -101,6 +101,22 @@ ORION_DEVICE void gemm_epilogue_tile(const GemmArgs& g, const f32x16& acc, int m
   if constexpr (EPI == EPI_BIAS_GELU) store(pk2, g.out2, g.ldo2);
 }
 
+// wait until at most N LDS reads are outstanding, with the fragments as "+v" operands (no
+// MFMA reading them can be scheduled before the wait)
+template <int N, int TJ>
+ORION_DEVICE void lds_wait_set(bf16x8 (&w)[4], bf16x8 (&x)[TJ]) {
+  if constexpr (TJ == 2) {
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(x[0]), "+v"(x[1]) : "n"(N));
+  } else {
+    static_assert(TJ == 4, "TJ in {2, 4}");
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(x[0]), "+v"(x[1]),
+                   "+v"(x[2]), "+v"(x[3])
+                 : "n"(N));
+  }
+}
+
 // K-stage depth BK and ring depth NS (LDS = NS * BK KB): {64, 2} or {32, 4}
 template <int BK, int NS>
 constexpr int gemm_lds() { return NS * 2 * 256 * BK * 2; }
@@ -117,20 +133,24 @@ ORION_DEVICE int img_swz(int row) {
   else return (row >> 2) & 3;
 }
 
-template <bool WKM, int EPI, int BK, int NS>
-__global__ __launch_bounds__(512, 1) void gemm_kernel(GemmArgs g) {
+// WM = waves along m: 4 -> 8 waves of 128 (n) x 64 (m) outputs (2 waves per SIMD); 2 -> 4
+// waves of 128 x 128 (one wave per SIMD, 256 accumulator registers in AGPRs: half the LDS
+// fragment reads per MFMA).
+template <bool WKM, int EPI, int BK, int NS, int WM = 4>
+__global__ __launch_bounds__(128 * WM, 1) void gemm_kernel(GemmArgs g) {
+  constexpr int NW = 2 * WM, TJ = 8 / WM;  // waves; 32-column m tiles per wave
   constexpr int IMG = 256 * BK, STAGE = 2 * IMG;
-  constexpr int NR = WKM ? 10 : 6;  // LDS reads per fragment set (X 2 b128, W 4 b128 | 8 tr)
+  constexpr int NR = (WKM ? 8 : 4) + TJ;  // LDS reads per fragment set (X TJ b128, W 4 b128 | 8 tr)
   constexpr int RPB = 1024 / (2 * BK);   // image rows per one-KB LDS-DMA block
   constexpr int CPR = BK / 8;            // 16-byte chunks per image row
-  constexpr int XB = 256 / RPB / 8;      // blocks per wave per [256][BK] image
-  constexpr int WB = (WKM ? BK / 2 : 256 / RPB) / 8;  // blocks per wave of the W image
+  constexpr int XB = 256 / RPB / NW;     // blocks per wave per [256][BK] image
+  constexpr int WB = (WKM ? BK / 2 : 256 / RPB) / NW;  // blocks per wave of the W image
   constexpr int PS = XB + WB;            // LDS-DMA instructions per stage per wave
-  static_assert(XB >= 1 && WB >= 1, "stage blocks must divide over the 8 waves");
+  static_assert(XB >= 1 && WB >= 1, "stage blocks must divide over the waves");
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h32 = lane >> 5, l32 = lane & 31;
-  const int wn = wv >> 2, wm = wv & 3;
+  const int wn = wv / WM, wm = wv % WM;
 
   // bijective XCD remap: blocks bid, bid + 8, ... share an XCD; give each XCD a contiguous
   // range of work ids (tiles of one X row panel are consecutive)
@@ -199,11 +219,11 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(GemmArgs g) {
       if (i % KSTEPS == s) issue_w(t, i);
   };
 
-  f32x16 acc[4][2];
+  f32x16 acc[4][TJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+    for (int j = 0; j < TJ; ++j) acc[i][j] = zero16();
 
   const int pre = min(nk, NS - 1);
   for (int st = 0; st < pre; ++st) issue(st);
@@ -230,11 +250,11 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(GemmArgs g) {
     if (refill && !(g.flags & 2)) issue(t + NS - 1);
     const bf16_t* Xs = smem + (t % NS) * STAGE;
     const bf16_t* Ws = Xs + IMG;
-    bf16x8 wf[2][4], xf[2][2];
+    bf16x8 wf[2][4], xf[2][TJ];
     auto fetch = [&](int s, int slot) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        xf[slot][j] = b128_read(Xs, img_off<BK>(wm * 64 + j * 32 + l32, 16 * s + 8 * h32));
+      for (int j = 0; j < TJ; ++j)
+        xf[slot][j] = b128_read(Xs, img_off<BK>(wm * (32 * TJ) + j * 32 + l32, 16 * s + 8 * h32));
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if constexpr (WKM)
@@ -250,14 +270,14 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(GemmArgs g) {
       if (refill && (g.flags & 2)) issue_step(t + NS - 1, s);
       if (s + 1 < BK / 16) {
         fetch(s + 1, cur ^ 1);
-        lds_wait_frags<NR, 4>(wf[cur], xf[cur]);  // step s = the older set
+        lds_wait_set<NR>(wf[cur], xf[cur]);  // step s = the older set
       } else {
-        lds_wait_frags<0, 4>(wf[cur], xf[cur]);
+        lds_wait_set<0>(wf[cur], xf[cur]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(wf[cur][i], xf[cur][j], acc[i][j]);
+        for (int j = 0; j < TJ; ++j) acc[i][j] = mfma32(wf[cur][i], xf[cur][j], acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -265,8 +285,8 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(GemmArgs g) {
   // epilogue: acc[i][j] = C^T tile; lane -> row m, register 4 g4 + e -> column
   // n = nb + 8 g4 + 4 h32 + e with nb the tile's first column
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int m = m0 + wm * 64 + j * 32 + l32;
+  for (int j = 0; j < TJ; ++j) {
+    const int m = m0 + wm * (32 * TJ) + j * 32 + l32;
     const int mc = min(m, g.M - 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) gemm_epilogue_tile<EPI>(g, acc[i][j], m, mc, n0 + wn * 128 + i * 32, h32);
@@ -414,30 +434,30 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 using namespace orion;
 
 // ORION_GEMM_CFG: 0 = BK 64 x 2 stages (default), 1 = ping-pong, 2 = BK 32 x 4-stage ring,
-// 3 = BK 32 x 5-stage ring (160 KB: three stages in flight).  All four measure within
-// +-5 % of each other on MI355X (docs/PERFORMANCE.md, "In-tree GEMM study").
+// 3 = BK 32 x 5-stage ring (160 KB: three stages in flight), 4/5/6 = 4 waves of 128 x 128
+// with BK 64 x 2 / BK 32 x 4 / BK 32 x 5 (docs/PERFORMANCE.md, "In-tree GEMM study").
 static int gemm_cfg() {
   static int c = -1;
   if (c < 0) {
     const char* e = getenv("ORION_GEMM_CFG");
     c = e ? atoi(e) : 0;
-    if (c < 0 || c > 3) c = 0;
+    if (c < 0 || c > 6) c = 0;
   }
   return c;
 }
 
-template <bool WKM, int EPI, int BK, int NS>
+template <bool WKM, int EPI, int BK, int NS, int WM = 4>
 static int gemm_launch_cfg(const GemmArgs& a, hipStream_t st) {
   static bool attr = false;
   constexpr int lds = gemm_lds<BK, NS>();
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_kernel<WKM, EPI, BK, NS>,
+    if (hipFuncSetAttribute((const void*)gemm_kernel<WKM, EPI, BK, NS, WM>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
       return -5;
     attr = true;
   }
   const int tiles_m = (a.M + 255) / 256;
-  gemm_kernel<WKM, EPI, BK, NS><<<tiles_m * a.tiles_n, 512, lds, st>>>(a);
+  gemm_kernel<WKM, EPI, BK, NS, WM><<<tiles_m * a.tiles_n, 128 * WM, lds, st>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -462,6 +482,9 @@ static int gemm_launch(const GemmArgs& a, hipStream_t st) {
     case 1: return gemm_launch_pp<WKM, EPI>(a, st);
     case 2: return gemm_launch_cfg<WKM, EPI, 32, 4>(a, st);
     case 3: return gemm_launch_cfg<WKM, EPI, 32, 5>(a, st);
+    case 4: return gemm_launch_cfg<WKM, EPI, 64, 2, 2>(a, st);
+    case 5: return gemm_launch_cfg<WKM, EPI, 32, 4, 2>(a, st);
+    case 6: return gemm_launch_cfg<WKM, EPI, 32, 5, 2>(a, st);
     default: return gemm_launch_cfg<WKM, EPI, 64, 2>(a, st);
   }
 }
