@@ -7,18 +7,11 @@ buffer, so there is no split/transpose/concat around the kernels.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
 from ._ext import C
-
-
-def deterministic() -> bool:
-    """Bitwise-reproducible attention gradients: ``ORION_DETERMINISTIC=1`` or
-    ``torch.use_deterministic_algorithms(True)`` select the split backward
-    (csrc/attn_bwd_split.hip: no atomics) at every head dim."""
-    return os.environ.get("ORION_DETERMINISTIC") == "1" or torch.are_deterministic_algorithms_enabled()
+from .determinism import deterministic
 
 
 def _bwd_flags() -> int:

@@ -26,13 +26,15 @@ import os
 import torch
 
 from ._ext import C
+from .determinism import deterministic
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
 # Linear-layer forward (x W^T [+ b]) and input gradient (dy W) run on hipBLASLt by default
 # (csrc/gemm.hip measures 0.75-1.05 PF/s against hipBLASLt's 0.9-1.4 on the GPT-2 shapes:
 # docs/PERFORMANCE.md).  The in-tree kernel is used when ORION_GEMM=hip, and always inside
 # a HIP-graph capture (``hip_gemms()``): its arguments are plain kernel arguments captured
-# in the graph node, with no library-side host state between replays.
+# in the graph node, with no library-side host state between replays -- and in the
+# deterministic mode (ops/determinism.py): one workgroup per output tile, no split-K.
 _GEMM_IMPL = os.environ.get("ORION_GEMM", "blas")  # "blas" | "hip"
 _FORCE_HIP = 0
 
@@ -51,7 +53,7 @@ def hip_gemms():
 
 
 def use_hip_gemm(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
-    if not (_FORCE_HIP or _GEMM_IMPL == "hip"):
+    if not (_FORCE_HIP or _GEMM_IMPL == "hip" or deterministic()):
         return False
     K = x.shape[-1]
     N = w.shape[1] if w_kmajor else w.shape[0]
@@ -103,7 +105,7 @@ def _blas_wins(n1: int, n2: int) -> bool:
     """hipBLASLt beats csrc/wgrad.hip by 5-12 % when both output dims are large (Llama-7B:
     12288/4096/22016/32000 x 4096 at 4k-16k tokens); the HIP kernel wins by 1.3-2x on the
     GPT-2 shapes and at 4096 x 11008 (scripts/bench_wgrad_llama.py, profiles/)."""
-    return n1 >= 4096 and n2 >= 4096 and n1 >= n2
+    return n1 >= 4096 and n2 >= 4096 and n1 >= n2 and not deterministic()
 
 
 def wgrad_into(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool,

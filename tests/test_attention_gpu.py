@@ -103,3 +103,25 @@ def test_cross_length_tk_ne_t(form, D, causal):
     want = _ref(q, k, v, do, causal)
     for name, a, b in zip(("o", "dq", "dk", "dv"), got, want):
         assert rel_err(a, b) < 3e-2, (name, rel_err(a, b))
+
+
+def test_deterministic_training_steps_are_bitwise_reproducible(monkeypatch):
+    """ORION_DETERMINISTIC=1 (ops/determinism.py): two fresh runs of three full training
+    steps (GPT-2 shape, 2 layers: split attention backward, in-tree GEMMs, fixed-order
+    reductions, fused AdamW) end with bit-identical losses and weights."""
+    from orion_amd.models.gpt2 import build_gpt2
+    from orion_amd.train.engine import Trainer, OptimConfig
+    monkeypatch.setenv("ORION_DETERMINISTIC", "1")
+    g = torch.Generator(device=DEV).manual_seed(7)
+    batches = [(torch.randint(0, 50257, (4, 256), device=DEV, generator=g),
+                torch.randint(0, 50257, (4, 256), device=DEV, generator=g)) for _ in range(3)]
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        m = build_gpt2("gpt2", n_layer=2, block_size=256).to(DEV)
+        tr = Trainer(m, OptimConfig(warmup_iters=1, lr_decay_iters=10, learning_rate=1e-3))
+        losses = [float(tr.step([b])) for b in batches]
+        runs.append((losses, tr.arena.params.clone(), tr.opt.master.clone()))
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2])
