@@ -30,6 +30,7 @@ typedef unsigned short bf16_t;  // raw bf16 bits
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(2))) long i64x2;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned short bf16x4;
 typedef __attribute__((ext_vector_type(8))) unsigned short bf16x8;

@@ -30,76 +30,9 @@
 //   * XCD-aware tile order: the tiles that share an X row panel are consecutive work ids,
 //     and consecutive work ids run on one XCD (bijective remap), so the panel is read
 //     from that XCD's L2.
-#include "mfma_lds.h"
+#include "gemm_common.h"
 
 namespace orion {
-
-enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3 };
-
-struct GemmArgs {
-  const bf16_t* X;  long ldx;   // [M][K] row-major
-  const bf16_t* W;  long ldw;   // NT: [N][K]; NN: [K][N]
-  bf16_t* out;      long ldo;   // [M][N]
-  const bf16_t* bias;           // [N]                      (EPI_BIAS, EPI_BIAS_GELU)
-  bf16_t* out2;     long ldo2;  // gelu(a), [M][N]          (EPI_BIAS_GELU)
-  const bf16_t* pre; long ldp;  // pre-activation a, [M][N] (EPI_GELU_BWD)
-  int M, N, K, tiles_n;
-  int flags;  // 1 = no LDS-DMA after the first stage (diagnostic), 2 = DMA spread over k steps
-};
-
-// One 32 x 32 accumulator of C^T (rows n = nb + (r&3) + 8(r>>2) + 4 h32, column = the
-// lane's output row m) through the epilogue and out as 16-byte row segments.
-template <int EPI>
-ORION_DEVICE void gemm_epilogue_tile(const GemmArgs& g, const f32x16& acc, int m, int mc, int nb,
-                                     int h32) {
-  unsigned pk[4][2], pk2[4][2];
-#pragma unroll
-  for (int g4 = 0; g4 < 4; ++g4) {
-    const int n = nb + 8 * g4 + 4 * h32;
-    const int nc = n < g.N ? n : 0;  // N % 8 == 0: a 4-run is all in or all out
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = acc[4 * g4 + e];
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
-      const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + nc);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += bf2f(b4[e]);
-    }
-    if constexpr (EPI == EPI_GELU_BWD) {
-      ORION_DASSERT(mc < g.M && nc + 4 <= g.N);
-      const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(g.pre + (long)mc * g.ldp + nc);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= gelu_tanh_grad_f(bf2f(a4[e]));
-    }
-    pk[g4][0] = pack_bf16x2(v[0], v[1]);
-    pk[g4][1] = pack_bf16x2(v[2], v[3]);
-    if constexpr (EPI == EPI_BIAS_GELU) {
-      pk2[g4][0] = pack_bf16x2(gelu_tanh_f(v[0]), gelu_tanh_f(v[1]));
-      pk2[g4][1] = pack_bf16x2(gelu_tanh_f(v[2]), gelu_tanh_f(v[3]));
-    }
-  }
-  // register pairs (g4, g4 + 1): after the swap lanes 0-31 hold columns 8 g4 .. 8 g4 + 7 and
-  // lanes 32-63 columns 8 g4 + 8 .. 8 g4 + 15 of the same row m
-  auto store = [&](unsigned (&pp)[4][2], bf16_t* base, long ld) {
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      unsigned a0 = pp[2 * pr][0], a1 = pp[2 * pr][1];
-      unsigned b0 = pp[2 * pr + 1][0], b1 = pp[2 * pr + 1][1];
-      const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-      const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-      a0 = r0[0]; b0 = r0[1]; a1 = r1[0]; b1 = r1[1];
-      const int n = nb + 16 * pr + 8 * h32;
-      if (m < g.M && n < g.N) {
-        ORION_DASSERT(n + 8 <= g.N && m >= 0);
-        uint4 w;
-        w.x = a0; w.y = a1; w.z = b0; w.w = b1;
-        *reinterpret_cast<uint4*>(base + (long)m * ld + n) = w;
-      }
-    }
-  };
-  store(pk, g.out, g.ldo);
-  if constexpr (EPI == EPI_BIAS_GELU) store(pk2, g.out2, g.ldo2);
-}
 
 // wait until at most N LDS reads are outstanding, with the fragments as "+v" operands (no
 // MFMA reading them can be scheduled before the wait)
@@ -433,17 +366,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 
 using namespace orion;
 
-// ORION_GEMM_CFG: 0 = BK 64 x 2 stages (default), 1 = ping-pong, 2 = BK 32 x 4-stage ring,
+// ORION_GEMM_CFG: 7 = phase-interleaved kernel (csrc/gemm_phased.hip, default), 0 = BK 64 x 2 stages, 1 = ping-pong, 2 = BK 32 x 4-stage ring,
 // 3 = BK 32 x 5-stage ring (160 KB: three stages in flight), 4/5/6 = 4 waves of 128 x 128
 // with BK 64 x 2 / BK 32 x 4 / BK 32 x 5 (docs/PERFORMANCE.md, "In-tree GEMM study").
-static int gemm_cfg() {
-  static int c = -1;
-  if (c < 0) {
-    const char* e = getenv("ORION_GEMM_CFG");
-    c = e ? atoi(e) : 0;
-    if (c < 0 || c > 6) c = 0;
-  }
-  return c;
+static int gemm_cfg() {  // read per call: microbenchmarks switch variants in one process
+  const char* e = getenv("ORION_GEMM_CFG");
+  const int c = e ? atoi(e) : 7;
+  return c < 0 || c > 7 ? 7 : c;
 }
 
 template <bool WKM, int EPI, int BK, int NS, int WM = 4>
@@ -506,6 +435,7 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
              (const bf16_t*)bias, (bf16_t*)out2, ldo2, (const bf16_t*)pre, ldp,
              M, N, K, (N + 255) / 256, 0};
   if (const char* e = getenv("ORION_GEMM_DIAG")) a.flags = atoi(e);
+  if (gemm_cfg() == 7 && gemm_phased_ok(a, wkm)) return gemm_phased(a, wkm, epi, st);
   switch (epi * 2 + (wkm ? 1 : 0)) {
     case EPI_STORE * 2 + 0: return gemm_launch<false, EPI_STORE>(a, st);
     case EPI_STORE * 2 + 1: return gemm_launch<true, EPI_STORE>(a, st);

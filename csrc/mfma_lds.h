@@ -111,13 +111,28 @@ ORION_DEVICE bf16x8 b128_read(const bf16_t* lds, int elem) {
   return r;
 }
 
-// tr_frag (above) on the asm read, [rows][128] image: element j of the lane's fragment is
+// tr_frag (above) on the asm read, [rows][D] image: element j of the lane's fragment is
 // image row rbase + (i>>2) + rstep*(j>>2) + ... (see tr_frag)
+template <int D = 128>
 ORION_DEVICE bf16x8 tr_frag_asm(const bf16_t* img, int rbase, int cbase, int lane, int rstep = 8) {
   const int g = lane >> 4, i = lane & 15;
   const int row = rbase + (i >> 2);
   const int col = cbase + 16 * (g & 1) + 4 * (i & 3);
-  return cat8(tr_read(img, loff<128>(row, col)), tr_read(img, loff<128>(row + rstep, col)));
+  return cat8(tr_read(img, loff<D>(row, col)), tr_read(img, loff<D>(row + rstep, col)));
+}
+
+// ---------------------------------------------------------------- buffer LDS-DMA
+// A raw buffer resource over `bytes` bytes at `base` (gfx9 dword-3 format) and the 16-byte
+// per-lane buffer_load_dwordx4 ... lds: LDS destination = wave-uniform `l` + 16 * lane;
+// byte address = base + voff (per lane, carries any swizzle) + soff (wave-uniform).  The
+// 32-bit per-lane offset costs one VGPR where global_load_lds needs a 64-bit pointer pair.
+ORION_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+ORION_DEVICE void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, bf16_t* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, soff,
+                                           0, 0);
 }
 
 // wait until at most N LDS reads are outstanding; the fragments are "+v" operands so

@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--M", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--check", action="store_true", help="compare outputs against torch")
+    ap.add_argument("--cfgs", default="7", help="comma list of ORION_GEMM_CFG variants to time (7 = phased)")
+    ap.add_argument("--square", type=int, default=0, help="also time an NT GEMM of this cube size")
+    ap.add_argument("--only", default="", help="comma list of shape names to run")
     a = ap.parse_args()
     from orion_amd.ops._ext import C, load_ext
     from orion_amd.tuning import use_tuned_gemms
@@ -55,8 +58,17 @@ def main():
               ("qkv_dgrad", "dgrad", 768, 2304, 0), ("attnproj_dgrad", "dgrad", 768, 768, 0),
               ("fc_dgrad", "dgrad", 768, 3072, 0), ("mlpproj_dgrad+gelu_bwd", "dgrad", 3072, 768, 3),
               ("lmhead_dgrad", "dgrad", 768, 50304, 0)]
+    if a.square:
+        shapes = [(f"square{a.square}", "fwd", a.square, a.square, 0)] + shapes
+    if a.only:
+        shapes = [sh for sh in shapes if sh[0] in a.only.split(",")]
+    cfgs = a.cfgs.split(",")
     tot = {"hip": 0.0, "blas": 0.0}
     for name, kind, N, K, epi in shapes:
+        if name.startswith("square"):
+            M = a.square
+        else:
+            M = a.M
         x = rnd(M, K)
         w = rnd(N, K) if kind == "fwd" else rnd(K, N)
         b = rnd(N) if epi in (1, 2) else None
@@ -74,15 +86,26 @@ def main():
                 blas = lambda: ops.bias_gelu_bwd(x @ w, pre, None, None)
             else:
                 blas = lambda: x @ w
-        t = timeit({"hip": hip, "blas": blas}, a.iters)
+        def with_cfg(c, f):
+            def run():
+                os.environ["ORION_GEMM_CFG"] = c
+                return f()
+            return run
+        fns = {f"hip{c}": with_cfg(c, hip) for c in cfgs}
+        fns["blas"] = blas
+        t = timeit(fns, a.iters)
+        t["hip"] = t[f"hip{cfgs[0]}"]
         flop = 2.0 * M * N * K
         rec = {"shape": name, "M": M, "N": N, "K": K, "epi": epi,
                "hip_ms": round(t["hip"], 4), "blas_ms": round(t["blas"], 4),
                "hip_TFs": round(flop / t["hip"] / 1e9, 1), "blas_TFs": round(flop / t["blas"] / 1e9, 1)}
+        for c in cfgs[1:]:
+            rec[f"cfg{c}_TFs"] = round(flop / t[f"hip{c}"] / 1e9, 1)
         if a.check:
             ref = (x.float() @ (w.float().t() if kind == "fwd" else w.float()))
             if b is not None:
                 ref = ref + b.float()
+            os.environ["ORION_GEMM_CFG"] = cfgs[0]
             got = hip()
             o = got[0].float()
             if epi == 3:
