@@ -7,7 +7,7 @@
 
 namespace orion {
 
-enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3 };
+enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3, EPI_WGRAD = 4 };
 
 struct GemmArgs {
   const bf16_t* X;  long ldx;   // [M][K] row-major
@@ -18,7 +18,12 @@ struct GemmArgs {
   const bf16_t* pre; long ldp;  // pre-activation a, [M][N] (EPI_GELU_BWD)
   int M, N, K, tiles_n;
   int flags;  // diagnostics (ORION_GEMM_DIAG): 1 = no LDS-DMA after the first stage; 2 = DMA spread over
-              // k steps (csrc/gemm.hip only)
+              // k steps (csrc/gemm.hip only); 8 = no C stores
+  // split-K (EPI_WGRAD, csrc/gemm_phased.hip): work item = (k chunk of kchunk rows, tile)
+  int kchunk, ksplit;
+  float* slabs;          // ksplit > 1: fp32 partial tiles [ksplit][M][N]
+  const float* scale;    // ksplit == 1: out (fp32 when out_f32, else bf16) = acc * *scale
+  int accumulate, out_f32;  //            (+ the value already in out when accumulate)
 };
 
 // Epilogue math of one 32 x 32 accumulator of C^T (rows n = nb + (r&3) + 8(r>>2) + 4 h32,
@@ -144,5 +149,7 @@ ORION_DEVICE void gemm_epilogue_lds(const GemmArgs& g, const f32x16 (&acc)[4][2]
 // csrc/gemm_phased.hip
 bool gemm_phased_ok(const GemmArgs& a, int wkm);
 int gemm_phased(const GemmArgs& a, int wkm, int epi, hipStream_t st);
+// weight gradient out[M][N] = sum_k X[k][M] W[k][N] (both operands k-major), split-K
+int gemm_phased_wgrad(const GemmArgs& a, hipStream_t st);
 
 }  // namespace orion

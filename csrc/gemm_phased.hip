@@ -63,7 +63,7 @@ ORION_DEVICE void ph_wait_lds(bf16x8 (&x)[4]) {
 
 }  // namespace
 
-template <bool WKM, int EPI>
+template <bool XKM, bool WKM, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   // once share GM X panels and ~32/GM W panels per k-tile in its L2.
   constexpr int GM = 4;
   const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
-  const int tiles_m = (g.M + 255) >> 8, T = tiles_m * g.tiles_n;
+  const int tiles_m = (g.M + 255) >> 8, tiles = tiles_m * g.tiles_n, T = tiles * g.ksplit;
   int wid, wstride, wend;
   if (nwg >= T) {
     const int qq = nwg >> 3, rr = nwg & 7;
@@ -91,36 +91,54 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
     wend = (int)((long)T * (xcd + 1) / 8);
   }
   if (wid >= wend) return;
-  auto tile_of = [&](int w, int& m0, int& n0) {
+  // work id -> (k chunk kc, tile): the tiles of one k chunk are consecutive work ids
+  auto tile_of = [&](int w, int& m0, int& n0, int& kc) {
+    kc = w / tiles;
+    w -= kc * tiles;
     const int grp_sz = GM * g.tiles_n, gidx = w / grp_sz, first_m = gidx * GM;
     const int gm = min(tiles_m - first_m, GM), in = w - gidx * grp_sz;
     m0 = (first_m + in % gm) * 256;
     n0 = (in / gm) * 256;
   };
-  int m0, n0;
-  tile_of(wid, m0, n0);
-  const int nk = g.K / PH_BK;
+  int m0, n0, kc;
+  tile_of(wid, m0, n0, kc);
+  int nk;  // k-tiles of the current work item
 
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.X, (unsigned)((long)g.M * g.ldx * 2));
-  const __amdgpu_buffer_rsrc_t rw =
-      make_rsrc(g.W, (unsigned)((WKM ? (long)g.K : (long)g.N) * g.ldw * 2));
-  const unsigned wstep = WKM ? (unsigned)(PH_BK * g.ldw * 2) : PH_BK * 2;  // bytes per k-tile
+  // operand buffer resources of the current work item, based at its k chunk (so 32-bit
+  // offsets suffice for any chunk < 4 GB), and bytes per k-tile
+  __amdgpu_buffer_rsrc_t rx, rw;
+  const unsigned xstep = XKM ? (unsigned)(PH_BK * g.ldx * 2) : PH_BK * 2;
+  const unsigned wstep = WKM ? (unsigned)(PH_BK * g.ldw * 2) : PH_BK * 2;
 
   // LDS-DMA: piece p (0 A, 1 B, 2 C, 3 D), this wave's blocks e = 0, 1 of its group's 8 (one
   // block = 8 image rows x 128 B = one wave instruction, lane -> row lane / 8, chunk lane % 8)
   unsigned vo[4][2];
   int ld[4][2];
   const int lr = lane >> 3, slot = lane & 7;
-  auto set_tile = [&](int m0, int n0) {
+  auto set_tile = [&](int m0, int n0, int kc) {
+    const int k0 = kc * g.kchunk, kr = min(g.kchunk, g.K - k0);
+    nk = kr / PH_BK;
+    if constexpr (XKM) rx = make_rsrc(g.X + (long)k0 * g.ldx, (unsigned)((long)kr * g.ldx * 2));
+    else rx = make_rsrc(g.X + k0, (unsigned)(((long)g.M * g.ldx - k0) * 2));
+    if constexpr (WKM) rw = make_rsrc(g.W + (long)k0 * g.ldw, (unsigned)((long)kr * g.ldw * 2));
+    else rw = make_rsrc(g.W + k0, (unsigned)(((long)g.N * g.ldw - k0) * 2));
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int b = 2 * wm + e;  // 0..7
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {  // X: B (m-tile 0 rows), C (m-tile 1 rows)
-        const int row0 = (2 * grp + (b >> 2)) * 64 + jj * 32 + (b & 3) * 8, row = row0 + lr;
-        const int ch = slot ^ swz<64>(row);
-        vo[1 + jj][e] = (unsigned)(((long)min(m0 + row, g.M - 1) * g.ldx + 8 * ch) * 2);
-        ld[1 + jj][e] = row0 * 64;
+        if constexpr (XKM) {
+          // [64 k][32 m] sub-image (jj, wm'), 64-byte rows, unswizzled; block = 16 k rows
+          const int wmp = 2 * grp + (b >> 2), kr0 = (b & 3) * 16, k = kr0 + (lane >> 2);
+          const int m = m0 + wmp * 64 + jj * 32 + 8 * (lane & 3);
+          vo[1 + jj][e] = (unsigned)(((long)k * g.ldx + min(m, g.M - 8)) * 2);
+          ld[1 + jj][e] = (jj * 4 + wmp) * 2048 + kr0 * 32;
+        } else {
+          const int row0 = (2 * grp + (b >> 2)) * 64 + jj * 32 + (b & 3) * 8, row = row0 + lr;
+          const int ch = slot ^ swz<64>(row);
+          vo[1 + jj][e] = (unsigned)(((long)min(m0 + row, g.M - 1) * g.ldx + 8 * ch) * 2);
+          ld[1 + jj][e] = row0 * 64;
+        }
       }
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {  // W: A (n-half 0), D (n-half 1) of this group
@@ -139,11 +157,11 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
       }
     }
   };
-  set_tile(m0, n0);
+  set_tile(m0, n0, kc);
   auto issue = [&](int p, int t) {
     bf16_t* base = smem + (t & 1) * PH_STAGE;
     const bool isx = p == 1 || p == 2;
-    const unsigned so = isx ? (unsigned)t * (PH_BK * 2) : (unsigned)t * wstep;
+    const unsigned so = (unsigned)t * (isx ? xstep : wstep);
     ORION_DASSERT(t < nk);
 #pragma unroll
     for (int e = 0; e < 2; ++e) blds16(isx ? rx : rw, vo[p][e], so, base + ld[p][e]);
@@ -157,9 +175,11 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) ko[s] = loff<64>(l32, 16 * s + 8 * h32);
   auto read_x = [&](bf16x8 (&x)[4], const bf16_t* Xs, int j) {
-    const bf16_t* b = Xs + (wm * 64 + j * 32) * 64;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) x[s] = b128_read(b, ko[s]);
+    for (int s = 0; s < 4; ++s) {
+      if constexpr (XKM) x[s] = tr_frag_asm_lin32(Xs + (j * 4 + wm) * 2048, 16 * s + 8 * h32, lane, 4);
+      else x[s] = b128_read(Xs + (wm * 64 + j * 32) * 64, ko[s]);
+    }
   };
   auto read_w = [&](bf16x8 (&w)[4], const bf16_t* Ws, int h, int i) {  // n-tile i of n-half h
 #pragma unroll
@@ -250,13 +270,14 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   const __amdgpu_buffer_rsrc_t ro2 =
       make_rsrc(EPI == EPI_BIAS_GELU ? g.out2 : g.out, (unsigned)((long)g.M * (EPI == EPI_BIAS_GELU ? g.ldo2 : g.ldo) * 2));
   constexpr int STORES = EPI == EPI_BIAS_GELU ? 32 : 16;  // buffer stores per wave per tile
+  const float wsc = (EPI == EPI_WGRAD && g.ksplit == 1 && g.scale) ? *g.scale : 1.f;
 
   prologue();
   bool first = true;
   while (true) {
     // A0 and B0 landed: 8 later prologue loads (4 if nk = 1) may be in flight, plus the
     // previous tile's STORES epilogue stores issued after them (vmcnt retires in order)
-    if (first) {
+    if (first || EPI == EPI_WGRAD) {  // (EPI_WGRAD's stores are not counted: wait for them)
       if (nk > 1) wait_vm_exact<8>();
       else wait_vm_exact<4>();
     } else {
@@ -295,13 +316,51 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
 
     // next tile's prologue DMA first, then this tile's epilogue: the loads land while the
     // epilogue runs and its stores drain under the next tile's first phases
-    const int cm0 = m0, cn0 = n0;
+    const int cm0 = m0, cn0 = n0, ckc = kc;
     wid += wstride;
     const bool more = wid < wend;
     if (more) {
-      tile_of(wid, m0, n0);
-      set_tile(m0, n0);
+      tile_of(wid, m0, n0, kc);
+      set_tile(m0, n0, kc);
       prologue();
+    }
+    if constexpr (EPI == EPI_WGRAD) {
+      // fp32 partial tile into slab ckc, or the final gradient (fp32 arena or bf16, scaled,
+      // optionally accumulated); lane = output row m, 4 consecutive columns per store
+      float* slab = g.ksplit > 1 ? g.slabs + (long)ckc * g.M * g.N : nullptr;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = cm0 + wm * 64 + j * 32 + l32;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const int n = cn0 + grp * 128 + i * 32 + 8 * g4 + 4 * h32;
+            if (m < g.M && n < g.N) {
+              const long o = (long)m * g.N + n;
+              f32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * g4 + e];
+              if (slab) {
+                *reinterpret_cast<f32x4*>(slab + o) = v;
+              } else if (g.out_f32) {
+                f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) + o);
+                v = v * wsc;
+                if (g.accumulate) v += *dst;
+                *dst = v;
+              } else {
+                bf16x4* dst = reinterpret_cast<bf16x4*>(g.out + o);
+                bf16x4 r, prev;
+                if (g.accumulate) prev = *dst;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) r[e] = f2bf(v[e] * wsc + (g.accumulate ? bf2f(prev[e]) : 0.f));
+                *dst = r;
+              }
+            }
+          }
+      }
+      if (!more) break;
+      continue;
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -337,11 +396,11 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   }
 }
 
-template <bool WKM, int EPI>
+template <bool XKM, bool WKM, int EPI>
 static int gemm_phased_launch(const GemmArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_phased_kernel<WKM, EPI>,
+    if (hipFuncSetAttribute((const void*)gemm_phased_kernel<XKM, WKM, EPI>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, PH_LDS_BYTES) != hipSuccess)
       return -5;
     attr = true;
@@ -354,9 +413,9 @@ static int gemm_phased_launch(const GemmArgs& a, hipStream_t st) {
       return -5;
     ncu = n >= 8 ? n & ~7 : 1 << 30;  // persistent grid: a multiple of 8 (one per XCD slot)
   }
-  const long tiles = (long)((a.M + 255) / 256) * a.tiles_n;
-  const int grid = (int)(tiles < ncu ? tiles : ncu);
-  gemm_phased_kernel<WKM, EPI><<<grid, 512, PH_LDS_BYTES, st>>>(a);
+  const long work = (long)((a.M + 255) / 256) * a.tiles_n * a.ksplit;
+  const int grid = (int)(work < ncu ? work : ncu);
+  gemm_phased_kernel<XKM, WKM, EPI><<<grid, 512, PH_LDS_BYTES, st>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -369,13 +428,20 @@ bool gemm_phased_ok(const GemmArgs& a, int wkm) {
   return xb < lim && wb < lim && ob < lim && o2 < lim;
 }
 
-int gemm_phased(const GemmArgs& a, int wkm, int epi, hipStream_t st) {
+int gemm_phased_wgrad(const GemmArgs& a, hipStream_t st) {
+  return gemm_phased_launch<true, true, EPI_WGRAD>(a, st);
+}
+
+int gemm_phased(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
+  GemmArgs a = a0;
+  a.kchunk = a.K;
+  a.ksplit = 1;
   switch (epi * 2 + (wkm ? 1 : 0)) {
-    case EPI_STORE * 2 + 0: return gemm_phased_launch<false, EPI_STORE>(a, st);
-    case EPI_STORE * 2 + 1: return gemm_phased_launch<true, EPI_STORE>(a, st);
-    case EPI_BIAS * 2 + 0: return gemm_phased_launch<false, EPI_BIAS>(a, st);
-    case EPI_BIAS_GELU * 2 + 0: return gemm_phased_launch<false, EPI_BIAS_GELU>(a, st);
-    case EPI_GELU_BWD * 2 + 1: return gemm_phased_launch<true, EPI_GELU_BWD>(a, st);
+    case EPI_STORE * 2 + 0: return gemm_phased_launch<false, false, EPI_STORE>(a, st);
+    case EPI_STORE * 2 + 1: return gemm_phased_launch<false, true, EPI_STORE>(a, st);
+    case EPI_BIAS * 2 + 0: return gemm_phased_launch<false, false, EPI_BIAS>(a, st);
+    case EPI_BIAS_GELU * 2 + 0: return gemm_phased_launch<false, false, EPI_BIAS_GELU>(a, st);
+    case EPI_GELU_BWD * 2 + 1: return gemm_phased_launch<false, true, EPI_GELU_BWD>(a, st);
     default: return -4;
   }
 }

@@ -121,6 +121,15 @@ ORION_DEVICE bf16x8 tr_frag_asm(const bf16_t* img, int rbase, int cbase, int lan
   return cat8(tr_read(img, loff<D>(row, col)), tr_read(img, loff<D>(row + rstep, col)));
 }
 
+// tr_frag_asm on an unswizzled [rows][32] image (64-byte rows: the 4 rows x 64 bytes a
+// 32-lane half reads are one 256-byte bank row, conflict-free without a swizzle)
+ORION_DEVICE bf16x8 tr_frag_asm_lin32(const bf16_t* img, int rbase, int lane, int rstep) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = rbase + (i >> 2);
+  const int col = 16 * (g & 1) + 4 * (i & 3);
+  return cat8(tr_read(img, row * 32 + col), tr_read(img, (row + rstep) * 32 + col));
+}
+
 // ---------------------------------------------------------------- buffer LDS-DMA
 // A raw buffer resource over `bytes` bytes at `base` (gfx9 dword-3 format) and the 16-byte
 // per-lane buffer_load_dwordx4 ... lds: LDS destination = wave-uniform `l` + 16 * lane;

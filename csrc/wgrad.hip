@@ -19,7 +19,7 @@
 //     on one XCD, so its 4 MB L2 serves the shared operand rows to all of them;
 //   * LDS-DMA staging into a 4-deep ring (see the kernel comment), one raw barrier
 //     per stage.
-#include "mfma_lds.h"
+#include "gemm_common.h"
 
 namespace orion {
 
@@ -180,21 +180,23 @@ struct WgCfg { int ks, ns, wm; };
 constexpr WgCfg WG_CFGS[] = {{2, 4, 4}, {2, 4, 2}, {4, 2, 2}, {2, 2, 4}};
 constexpr int WG_NCFG = sizeof(WG_CFGS) / sizeof(WG_CFGS[0]);
 
+// ORION_WGRAD_CFG: 7 = the phase-interleaved kernel (csrc/gemm_phased.hip, default), 0-3 =
+// wgrad_kernel configurations of WG_CFGS (read per call: microbenchmarks switch in-process)
+constexpr int WG_PHASED = 7;
 static int wg_cfg() {
-  static int c = -1;
-  if (c < 0) {
-    const char* e = getenv("ORION_WGRAD_CFG");
-    c = e ? atoi(e) : 0;
-    if (c < 0 || c >= WG_NCFG) c = 0;
-  }
-  return c;
+  const char* e = getenv("ORION_WGRAD_CFG");
+  const int c = e ? atoi(e) : WG_PHASED;
+  return c == WG_PHASED || (c >= 0 && c < WG_NCFG) ? c : WG_PHASED;
 }
 
 }  // namespace orion
 
 using namespace orion;
 
-static int wg_bk() { return 16 * WG_CFGS[wg_cfg()].ks; }
+static int wg_bk() {
+  const int c = wg_cfg();
+  return c == WG_PHASED ? 64 : 16 * WG_CFGS[c].ks;
+}
 
 // Split count: minimise (rounds of one-workgroup-per-CU) x (rows per workgroup) plus
 // the fp32 slab round trip, in units of rows of work.
@@ -229,6 +231,7 @@ int orion_wgrad_effective_splits(int M, int S) {
 }
 
 int orion_wgrad_lds() {
+  if (wg_cfg() == WG_PHASED) return 128 * 1024;
   const WgCfg c = WG_CFGS[wg_cfg()];
   return c.ns * c.ks * 16 * 128 * 4 * (int)sizeof(bf16_t);
 }
@@ -248,6 +251,27 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   if (S > 1 && !slabs) return -4;
   const int t1 = (N1 + 255) / 256, t2 = (N2 + 255) / 256;
   const int ntiles = t1 * t2;
+  if (wg_cfg() == WG_PHASED) {
+    GemmArgs a{};
+    a.X = (const bf16_t*)A;  // [M tokens][N1]: the k-major "X" operand, rows of out = N1
+    a.ldx = lda;
+    a.W = (const bf16_t*)B;  // [M tokens][N2]
+    a.ldw = ldb;
+    a.out = (bf16_t*)out;
+    a.ldo = N2;
+    a.M = N1;
+    a.N = N2;
+    a.K = M;
+    a.tiles_n = t2;
+    a.kchunk = chunk;
+    a.ksplit = S;
+    a.slabs = S > 1 ? slabs : nullptr;
+    a.scale = scale;
+    a.accumulate = accumulate;
+    a.out_f32 = out_f32;
+    if ((long)chunk * (lda > ldb ? lda : ldb) * 2 >= 0xFFFFFF00L) return -1;
+    return gemm_phased_wgrad(a, st);
+  }
   const int lds = orion_wgrad_lds();
   auto Ab = (const bf16_t*)A;
   auto Bb = (const bf16_t*)B;
