@@ -23,6 +23,8 @@ x, w, b = r(300, 192), r(264, 192), r(264)
 ops.gemm(x, w, False, 2, b, None)
 ops.gemm(r(300, 256), r(256, 200), True, 3, None, r(300, 200))
 ops.wgrad(r(320, 264), r(320, 136), None, 0)
+ops.wgrad(r(8192, 264), r(8192, 136), None, 0)  # split-K work items
+ops.gemm(r(777, 128), r(50304, 128), False, 0, None, None)  # persistent tile walk
 q, k, v, do = r(1, 200, 4, 128), r(1, 328, 2, 128), r(1, 328, 2, 128), r(1, 200, 4, 128)
 o, lse = ops.attn_fwd(q, k, v, True, 1 / math.sqrt(128))
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)

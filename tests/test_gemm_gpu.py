@@ -1,6 +1,8 @@
-"""csrc/gemm.hip (forward NT / input-gradient NN GEMMs with fused epilogues) against an fp32
-PyTorch reference, including ragged M and N (partial 256 x 256 tiles) and the epilogues
-(bias, bias + GELU with the pre-activation output, GELU backward)."""
+"""The linear-layer GEMMs (csrc/gemm_phased.hip by default, csrc/gemm.hip's 2-stage kernel
+under ORION_GEMM_CFG=0; forward NT / input-gradient NN with fused epilogues) against an fp32
+PyTorch reference, including ragged M and N (partial 256 x 256 tiles), more tiles than CUs
+(the persistent tile walk: 777 x 50304) and the epilogues (bias, bias + GELU with the
+pre-activation output, GELU backward)."""
 import pytest
 import torch
 
@@ -77,3 +79,31 @@ def test_gemm_batched_input_shape_and_strided_rows():
     xs = big[:, 768:1536]
     out2, _ = _C().gemm(xs, w[:, :256].contiguous().repeat(1, 3), False, 0, None, None)
     assert rel_err(out2, xs.float() @ w[:, :256].float().repeat(1, 3).t()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 264, 128), (1000, 768, 768), (777, 50304, 128)])
+@pytest.mark.parametrize("wkm", [False, True])
+def test_gemm_two_stage_kernel(M, N, K, wkm, monkeypatch):
+    """csrc/gemm.hip's 2-stage kernel (ORION_GEMM_CFG=0, read per call)."""
+    monkeypatch.setenv("ORION_GEMM_CFG", "0")
+    g = torch.Generator(device=DEV).manual_seed(M + 3 * N + K)
+    x = _rnd(g, M, K)
+    w = _rnd(g, K, N) if wkm else _rnd(g, N, K)
+    out, _ = _C().gemm(x, w, wkm, 0, None, None)
+    assert rel_err(out, x.float() @ (w.float() if wkm else w.float().t())) < 1e-2
+
+
+@pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768)])
+@pytest.mark.parametrize("cfg", ["7", "0"])
+@pytest.mark.parametrize("acc", [False, True])
+def test_wgrad_phased_and_two_stage_into_fp32(M, N1, N2, cfg, acc, monkeypatch):
+    """Weight gradients on the phased kernel (split-K work items, fp32 slabs) and on
+    csrc/wgrad.hip (ORION_WGRAD_CFG=0) into an fp32 arena slice, overwrite and accumulate."""
+    monkeypatch.setenv("ORION_WGRAD_CFG", cfg)
+    g = torch.Generator(device=DEV).manual_seed(M + N1)
+    dy, x = _rnd(g, M, N1), _rnd(g, M, N2)
+    out = torch.randn(N1, N2, device=DEV, generator=g)
+    base = out.clone()
+    _C().wgrad_into(dy, x, None, out, acc, 0)
+    want = dy.float().t() @ x.float() + (base if acc else 0)
+    assert rel_err(out, want) < 1e-4
