@@ -435,6 +435,7 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
              (const bf16_t*)bias, (bf16_t*)out2, ldo2, (const bf16_t*)pre, ldp,
              M, N, K, (N + 255) / 256, 0};
   if (const char* e = getenv("ORION_GEMM_DIAG")) a.flags = atoi(e);
+  if ((a.flags & 4) && epi == EPI_STORE) a.slabs = (float*)pre;  // slot stamps (diagnostic)
   if (gemm_cfg() == 7 && gemm_phased_ok(a, wkm)) return gemm_phased(a, wkm, epi, st);
   switch (epi * 2 + (wkm ? 1 : 0)) {
     case EPI_STORE * 2 + 0: return gemm_launch<false, EPI_STORE>(a, st);

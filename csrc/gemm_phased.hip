@@ -63,7 +63,10 @@ ORION_DEVICE void ph_wait_lds(bf16x8 (&x)[4]) {
 
 }  // namespace
 
-template <bool XKM, bool WKM, int EPI>
+// STAMPS (diagnostic instantiation, ORION_GEMM_DIAG=4 with a stamp buffer, EPI_STORE only):
+// workgroup 0 records s_memtime per wave at each slot boundary into g.slabs as u64
+// [wave][1024] (scripts/gemm_stamps.py); no effect on results.
+template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
 __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -190,6 +193,14 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
         w[s] = b128_read(Ws + (grp * 128 + h * 64 + i * 32) * 64, ko[s]);
     }
   };
+  int nstamp = 0;
+  auto stamp = [&] {
+    if constexpr (STAMPS) {
+      if (blockIdx.x == 0 && lane == 0 && nstamp < 1024)
+        reinterpret_cast<unsigned long*>(g.slabs)[wv * 1024 + nstamp] = __builtin_amdgcn_s_memtime();
+      ++nstamp;
+    }
+  };
   auto mma = [&](bf16x8 (&w)[2][4], bf16x8 (&x)[4], int i0, int j) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -208,6 +219,7 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
     const bf16_t* Xs = smem + (t & 1) * PH_STAGE;
     const bf16_t* Ws = Xs + PH_IMG;
     // ---- READ slot
+    stamp();  // R: slot start (after the barrier)
     if constexpr (Q == 0) {
       read_w(W0[0], Ws, 0, 0);
       read_w(W0[1], Ws, 0, 1);
@@ -231,18 +243,24 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
       ph_wait_lds(W0[0], X0);
       ph_wait_lds(W0[1]);
       __builtin_amdgcn_sched_barrier(0);
+      stamp();  // S: fragments landed, MFMAs start
       mma(W0, X0, 0, 0);
     } else if constexpr (Q == 1) {
       ph_wait_lds(X1);
       __builtin_amdgcn_sched_barrier(0);
+      stamp();
       mma(W0, X1, 0, 1);
     } else if constexpr (Q == 2) {
       ph_wait_lds(W1[0], W1[1]);
       __builtin_amdgcn_sched_barrier(0);
+      stamp();
       mma(W1, X0, 2, 0);
     } else {
+      __builtin_amdgcn_sched_barrier(0);
+      stamp();
       mma(W1, X1, 2, 1);
     }
+    stamp();  // E: MFMAs issued
     ph_barrier();
   };
   using I0 = std::integral_constant<int, 0>;
@@ -396,11 +414,11 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   }
 }
 
-template <bool XKM, bool WKM, int EPI>
-static int gemm_phased_launch(const GemmArgs& a, hipStream_t st) {
+template <bool XKM, bool WKM, int EPI, bool STAMPS>
+static int gemm_phased_launch_s(const GemmArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_phased_kernel<XKM, WKM, EPI>,
+    if (hipFuncSetAttribute((const void*)gemm_phased_kernel<XKM, WKM, EPI, STAMPS>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, PH_LDS_BYTES) != hipSuccess)
       return -5;
     attr = true;
@@ -415,8 +433,16 @@ static int gemm_phased_launch(const GemmArgs& a, hipStream_t st) {
   }
   const long work = (long)((a.M + 255) / 256) * a.tiles_n * a.ksplit;
   const int grid = (int)(work < ncu ? work : ncu);
-  gemm_phased_kernel<XKM, WKM, EPI><<<grid, 512, PH_LDS_BYTES, st>>>(a);
+  gemm_phased_kernel<XKM, WKM, EPI, STAMPS><<<grid, 512, PH_LDS_BYTES, st>>>(a);
   return (int)hipGetLastError();
+}
+
+template <bool XKM, bool WKM, int EPI>
+static int gemm_phased_launch(const GemmArgs& a, hipStream_t st) {
+  if constexpr (!XKM && EPI == EPI_STORE) {
+    if ((a.flags & 4) && a.slabs) return gemm_phased_launch_s<XKM, WKM, EPI, true>(a, st);
+  }
+  return gemm_phased_launch_s<XKM, WKM, EPI, false>(a, st);
 }
 
 // Requirements beyond orion_gemm's: every operand and output byte offset fits in 32 bits

@@ -22,6 +22,7 @@ a = ap.parse_args()
 load_ext(required=True)
 ops = C()
 g = torch.Generator(device="cuda").manual_seed(0)
+summary = {}
 for sh in a.shapes.split(","):
     M, N, K, wkm = (int(v) for v in sh.split("x"))
     x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
@@ -42,5 +43,7 @@ for sh in a.shapes.split(","):
     for (c, d), v in ts.items():
         ms = sorted(v)[len(v) // 2]
         rec[f"cfg{c}_diag{d}_TFs"] = round(2.0 * M * N * K / ms / 1e9, 1)
+        summary[f"{sh}_c{c}d{d}"] = rec[f"cfg{c}_diag{d}_TFs"]
     print(json.dumps(rec), flush=True)
+print(json.dumps(summary))  # one line with every shape (scripts/ab.sh prints the last line)
 os.environ["ORION_GEMM_DIAG"] = "0"
