@@ -489,14 +489,24 @@ std::tuple<Tensor, Tensor, Tensor> add_rmsnorm_fwd(const Tensor& x, const Tensor
   return {sum, y, rstd};
 }
 
+// dw_out: the weight's slice of the gradient arena (fp32 or bf16, C elements, written in
+// place: ops/grad_sink.py) -- returned as dw; else a fresh tensor of w's dtype.
 std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w,
-                                       const Tensor& rstd, const c10::optional<Tensor>& dres) {
+                                       const Tensor& rstd, const c10::optional<Tensor>& dres,
+                                       const c10::optional<Tensor>& dw_out) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto dyc = dy.contiguous(), xc = x.contiguous();
   const int C = x.size(-1);
   const int rows = x.numel() / C;
   auto dx = at::empty_like(xc);
-  auto dw = at::empty({C}, w.options());
+  Tensor dw;
+  if (dw_out.has_value() && dw_out->defined()) {
+    check_grad_out(*dw_out, "dw_out");
+    TORCH_CHECK(dw_out->is_contiguous() && dw_out->numel() == C, "rmsnorm_bwd: dw_out must be C contiguous elements");
+    dw = *dw_out;
+  } else {
+    dw = at::empty({C}, w.options());
+  }
   auto part = at::empty({((long)orion_rmsnorm_bwd_blocks(rows) + 32) * C}, x.options().dtype(at::kFloat));
   Tensor drc;
   if (dres.has_value() && dres->defined()) {
@@ -506,7 +516,7 @@ std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const 
   check_launch(orion_rmsnorm_bwd(dyc.data_ptr(), xc.data_ptr(), w.contiguous().data_ptr(),
                                  rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr(),
                                  part.data_ptr<float>(), rows, C,
-                                 drc.defined() ? drc.data_ptr() : nullptr, 0, cur_stream()),
+                                 drc.defined() ? drc.data_ptr() : nullptr, is_f32(dw) ? 1 : 0, cur_stream()),
                "rmsnorm_bwd");
   return {dx, dw};
 }
@@ -667,7 +677,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
-  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None, Tensor(a!)? dw_out=None) -> (Tensor, Tensor)");
   m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int pos0, float sign) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int pos0, float sign) -> ()");

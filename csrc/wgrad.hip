@@ -183,18 +183,21 @@ constexpr int WG_NCFG = sizeof(WG_CFGS) / sizeof(WG_CFGS[0]);
 // ORION_WGRAD_CFG: 7 = the phase-interleaved kernel (csrc/gemm_phased.hip, default), 0-3 =
 // wgrad_kernel configurations of WG_CFGS (read per call: microbenchmarks switch in-process)
 constexpr int WG_PHASED = 7;
-static int wg_cfg() {
+// (the phased kernel stages 64-token k-tiles: token counts that are not a multiple of 64
+// take wgrad_kernel's default configuration, which stages 32)
+static int wg_cfg(int M) {
   const char* e = getenv("ORION_WGRAD_CFG");
-  const int c = e ? atoi(e) : WG_PHASED;
-  return c == WG_PHASED || (c >= 0 && c < WG_NCFG) ? c : WG_PHASED;
+  int c = e ? atoi(e) : WG_PHASED;
+  if (!(c == WG_PHASED || (c >= 0 && c < WG_NCFG))) c = WG_PHASED;
+  return c == WG_PHASED && M % 64 ? 0 : c;
 }
 
 }  // namespace orion
 
 using namespace orion;
 
-static int wg_bk() {
-  const int c = wg_cfg();
+static int wg_bk(int M) {
+  const int c = wg_cfg(M);
   return c == WG_PHASED ? 64 : 16 * WG_CFGS[c].ks;
 }
 
@@ -206,7 +209,7 @@ int orion_wgrad_splits(int M, int N1, int N2) {
   double best = 1e30;
   int bestS = 1;
   for (int S = 1; S <= 32; ++S) {
-    const int BK = wg_bk();
+    const int BK = wg_bk(M);
     const int chunk = ((M / BK + S - 1) / S) * BK;
     if (chunk < 8 * BK && S > 1) break;
     const int Se = (M + chunk - 1) / chunk;
@@ -225,14 +228,14 @@ int orion_wgrad_splits(int M, int N1, int N2) {
 // number of k-chunks actually produced when S are requested (chunks are whole stages)
 int orion_wgrad_effective_splits(int M, int S) {
   if (S < 1) S = 1;
-  const int BK = wg_bk();
+  const int BK = wg_bk(M);
   const int chunk = ((M / BK + S - 1) / S) * BK;
   return chunk > 0 ? (M + chunk - 1) / chunk : 1;
 }
 
-int orion_wgrad_lds() {
-  if (wg_cfg() == WG_PHASED) return 128 * 1024;
-  const WgCfg c = WG_CFGS[wg_cfg()];
+static int wgrad_lds(int M) {
+  if (wg_cfg(M) == WG_PHASED) return 128 * 1024;
+  const WgCfg c = WG_CFGS[wg_cfg(M)];
   return c.ns * c.ks * 16 * 128 * 4 * (int)sizeof(bf16_t);
 }
 
@@ -242,7 +245,7 @@ int orion_wgrad_lds() {
 int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1, int N2, int S,
                 float* slabs, void* out, const float* scale, int accumulate, int out_f32,
                 hipStream_t st) {
-  const int BK = wg_bk();
+  const int BK = wg_bk(M);
   if (M % BK || N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || N1 < 8 || N2 < 8) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -2;
   const int chunk = ((M / BK + S - 1) / S) * BK;
@@ -251,7 +254,7 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   if (S > 1 && !slabs) return -4;
   const int t1 = (N1 + 255) / 256, t2 = (N2 + 255) / 256;
   const int ntiles = t1 * t2;
-  if (wg_cfg() == WG_PHASED) {
+  if (wg_cfg(M) == WG_PHASED) {
     GemmArgs a{};
     a.X = (const bf16_t*)A;  // [M tokens][N1]: the k-major "X" operand, rows of out = N1
     a.ldx = lda;
@@ -272,7 +275,7 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
     if ((long)chunk * (lda > ldb ? lda : ldb) * 2 >= 0xFFFFFF00L) return -1;
     return gemm_phased_wgrad(a, st);
   }
-  const int lds = orion_wgrad_lds();
+  const int lds = wgrad_lds(M);
   auto Ab = (const bf16_t*)A;
   auto Bb = (const bf16_t*)B;
   float* sl = S > 1 ? slabs : nullptr;
@@ -289,7 +292,7 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
                                                           ntiles, chunk, sl, out, scale,        \
                                                           accumulate, out_f32);                 \
   }
-  switch (wg_cfg()) {
+  switch (wg_cfg(M)) {
     case 0: WG_LAUNCH(wgrad_kernel, 2, 4, 4) break;  // measured best on MI355X (16 waves, 122 VGPR)
     case 1: WG_LAUNCH(wgrad_kernel, 2, 4, 2) break;
     case 2: WG_LAUNCH(wgrad_kernel, 4, 2, 2) break;

@@ -77,7 +77,7 @@ def linear_dgrad(dy, w):
     return dy @ w
 
 _FORCE = os.environ.get("ORION_WGRAD_SPLITS")
-_IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/wgrad.hip) | "bmm"
+_IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/gemm_phased.hip) | "blas" | "bmm"
 
 
 def _hip_ok(dy, x):
@@ -102,10 +102,12 @@ def wgrad_splits(M: int, n1: int, n2: int) -> int:
 
 
 def _blas_wins(n1: int, n2: int) -> bool:
-    """hipBLASLt beats csrc/wgrad.hip by 5-12 % when both output dims are large (Llama-7B:
-    12288/4096/22016/32000 x 4096 at 4k-16k tokens); the HIP kernel wins by 1.3-2x on the
-    GPT-2 shapes and at 4096 x 11008 (scripts/bench_wgrad_llama.py, profiles/)."""
-    return n1 >= 4096 and n2 >= 4096 and n1 >= n2 and not deterministic()
+    """hipBLASLt for the weight gradient only when asked (ORION_WGRAD=blas): the phased kernel
+    of csrc/gemm_phased.hip beats it on every measured shape -- GPT-2 (1.3-2x) and the
+    Llama-7B shapes at 16k tokens (12288/4096/22016/32000 x 4096 and 4096 x 11008: 9.8 vs
+    10.75 ms in total, profiles/gemm_study/bench_wgrad_llama_shapes.log), where csrc/wgrad.hip
+    used to lose by 5-12 %."""
+    return _IMPL == "blas" and not deterministic()
 
 
 def wgrad_into(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool,

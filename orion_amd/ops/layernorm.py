@@ -154,13 +154,16 @@ class _RMSNorm(torch.autograd.Function):
         y, rstd = C().rmsnorm_fwd(xb, _bf16(w), float(eps))
         ctx.save_for_backward(xb, w, rstd)
         ctx.x_dtype = x.dtype
+        ctx.params = (w,)
         return y.view(x.shape).to(x.dtype)
 
     @staticmethod
     def backward(ctx, dy):
         xb, w, rstd = ctx.saved_tensors
-        dx, dw = C().rmsnorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), rstd, None)
-        return dx.view(xb.shape).to(ctx.x_dtype), dw.to(w.dtype), None
+        (sw,) = _claim(ctx.params)  # dw straight into the gradient arena (ops/grad_sink.py)
+        dx, dw = C().rmsnorm_bwd(_bf16(dy.contiguous()), xb, _bf16(w), rstd, None, _view(sw))
+        _notify(sw)
+        return dx.view(xb.shape).to(ctx.x_dtype), _grad(_unless(dw, sw), w.dtype), None
 
 
 def rms_norm_hip(x, weight, eps=1e-5):
@@ -174,6 +177,7 @@ class _AddRMSNorm(torch.autograd.Function):
     def forward(ctx, x, r, w, eps):
         s, y, rstd = C().add_rmsnorm_fwd(x, r, _bf16(w), float(eps))
         ctx.save_for_backward(s, w, rstd)
+        ctx.params = (w,)
         return s.view(x.shape), y.view(x.shape)
 
     @staticmethod
@@ -182,9 +186,11 @@ class _AddRMSNorm(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros_like(s)
         dres = None if ds is None else ds.contiguous()
-        dx, dw = C().rmsnorm_bwd(dy.contiguous(), s, _bf16(w), rstd, dres)
+        (sw,) = _claim(ctx.params)
+        dx, dw = C().rmsnorm_bwd(dy.contiguous(), s, _bf16(w), rstd, dres, _view(sw))
+        _notify(sw)
         dx = dx.view(s.shape)
-        return dx, dx, dw.to(w.dtype), None
+        return dx, dx, _grad(_unless(dw, sw), w.dtype), None
 
 
 def add_rms_norm_hip(x, r, weight, eps=1e-5):

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--cfgs", default="7", help="comma list of ORION_GEMM_CFG variants to time (7 = phased)")
     ap.add_argument("--square", type=int, default=0, help="also time an NT GEMM of this cube size")
     ap.add_argument("--only", default="", help="comma list of shape names to run")
+    ap.add_argument("--llama", action="store_true", help="Llama-2-7B shapes (M = 16,384 tokens) instead")
     a = ap.parse_args()
     from orion_amd.ops._ext import C, load_ext
     from orion_amd.tuning import use_tuned_gemms
@@ -58,6 +59,13 @@ def main():
               ("qkv_dgrad", "dgrad", 768, 2304, 0), ("attnproj_dgrad", "dgrad", 768, 768, 0),
               ("fc_dgrad", "dgrad", 768, 3072, 0), ("mlpproj_dgrad+gelu_bwd", "dgrad", 3072, 768, 3),
               ("lmhead_dgrad", "dgrad", 768, 50304, 0)]
+    if a.llama:
+        shapes = [("l_qkv_fwd", "fwd", 12288, 4096, 0), ("l_o_fwd", "fwd", 4096, 4096, 0),
+                  ("l_gateup_fwd", "fwd", 22016, 4096, 0), ("l_down_fwd", "fwd", 4096, 11008, 0),
+                  ("l_lmhead_fwd", "fwd", 32000, 4096, 0),
+                  ("l_qkv_dgrad", "dgrad", 4096, 12288, 0), ("l_o_dgrad", "dgrad", 4096, 4096, 0),
+                  ("l_gateup_dgrad", "dgrad", 4096, 22016, 0), ("l_down_dgrad", "dgrad", 11008, 4096, 0),
+                  ("l_lmhead_dgrad", "dgrad", 4096, 32000, 0)]
     if a.square:
         shapes = [(f"square{a.square}", "fwd", a.square, a.square, 0)] + shapes
     if a.only:

@@ -18,6 +18,7 @@ ap.add_argument("--cfgs", default="7,0")
 ap.add_argument("--iters", type=int, default=15)
 ap.add_argument("--M", type=int, default=65536)
 ap.add_argument("--shapes", default="768x768,2304x768,3072x768,768x3072,50304x768")
+ap.add_argument("--blas", action="store_true", help="also time hipBLASLt (fp32-output mm into the slice)")
 a = ap.parse_args()
 load_ext(required=True)
 ops = C()
@@ -30,13 +31,16 @@ for sh in a.shapes.split(","):
     out = torch.empty(n1, n2, device="cuda", dtype=torch.float32)
     ref = dy.float().t() @ x.float()
     rec = {"shape": sh}
-    ts = {c: [] for c in a.cfgs.split(",")}
+    ts = {c: [] for c in a.cfgs.split(",") + (["blas"] if a.blas else [])}
     for it in range(a.iters + 3):
         for c in ts:
-            os.environ["ORION_WGRAD_CFG"] = c
+            os.environ["ORION_WGRAD_CFG"] = c if c != "blas" else "7"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            ops.wgrad_into(dy, x, None, out, False, 0)
+            if c == "blas":
+                torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)
+            else:
+                ops.wgrad_into(dy, x, None, out, False, 0)
             e1.record()
             e1.synchronize()
             if it >= 3:

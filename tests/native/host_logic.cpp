@@ -31,7 +31,7 @@ static int failures = 0;
 
 int main() {
   // split-K planning over the shapes the models produce (and odd ones)
-  const int Ms[] = {32, 256, 4096, 8192, 16384, 65536, 131072, 262144};
+  const int Ms[] = {32, 96, 256, 4096, 8192, 8224, 16384, 65536, 131072, 262144};
   const int Ns[] = {8, 64, 264, 768, 1000, 2304, 3072, 4096, 11008, 50304};
   for (int M : Ms)
     for (int n1 : Ns)

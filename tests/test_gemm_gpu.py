@@ -93,12 +93,13 @@ def test_gemm_two_stage_kernel(M, N, K, wkm, monkeypatch):
     assert rel_err(out, x.float() @ (w.float() if wkm else w.float().t())) < 1e-2
 
 
-@pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768)])
+@pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768), (8224, 200, 264)])
 @pytest.mark.parametrize("cfg", ["7", "0"])
 @pytest.mark.parametrize("acc", [False, True])
 def test_wgrad_phased_and_two_stage_into_fp32(M, N1, N2, cfg, acc, monkeypatch):
     """Weight gradients on the phased kernel (split-K work items, fp32 slabs) and on
-    csrc/wgrad.hip (ORION_WGRAD_CFG=0) into an fp32 arena slice, overwrite and accumulate."""
+    csrc/wgrad.hip (ORION_WGRAD_CFG=0) into an fp32 arena slice, overwrite and accumulate
+    (8224 tokens: not a multiple of 64, so the phased default hands over to csrc/wgrad.hip)."""
     monkeypatch.setenv("ORION_WGRAD_CFG", cfg)
     g = torch.Generator(device=DEV).manual_seed(M + N1)
     dy, x = _rnd(g, M, N1), _rnd(g, M, N2)
