@@ -104,6 +104,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
   float m = -1e30f, lsum = 0.f;
   const int myq = qw0 + l32;
 
+  // Staging (issue early, write late): tile t+1 sits in registers while tile t is computed;
+  // right after the barrier that ends tile t-1 it is written to the LDS buffer tile t-1 used,
+  // and tile t+2's loads are issued -- so the LDS writes overlap this tile's MFMAs instead
+  // of delaying the barrier, and each load has a whole tile of compute to land.
   gload(0);
   swrite(0);
   // Retire EVERY prologue load (Q fragments included) with an s_waitcnt the compiler's
@@ -111,9 +115,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
   // header and makes the first QK^T MFMAs of every tile wait vmcnt(3..0) -- i.e. on the
   // NEXT tile's prefetch -- exposing a full HBM round trip per tile.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  if (ntiles > 1) gload(1);
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) gload(t + 1);
+    if (t + 1 < ntiles) swrite((t + 1) & 1);
+    if (t + 2 < ntiles) gload(t + 2);
     const int k0 = t * BN;
     const bf16_t* Ks = smem + (t & 1) * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
@@ -148,9 +154,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float alpha = __builtin_amdgcn_exp2f((m - mx) * c);
-      m = mx;
-      const float mc = mx * c;
+      // deferred rescale: keep the running max while no row of the wave grew by more than
+      // 8 (log2 units), so P stays <= 2^8 (exact in fp32 sums, bf16-rounded like any P); the
+      // O / l rescale pass then runs only on the tiles that raise a row's max that much
+      float alpha = 1.f;
+      if (__any((mx - m) * c > 8.f)) {
+        alpha = __builtin_amdgcn_exp2f((m - mx) * c);
+        m = mx;
+#pragma unroll
+        for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+      }
+      const float mc = m * c;
       float ps = 0.f;
       bf16x8 pf[4];
 #pragma unroll
@@ -165,10 +181,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
           }
       lsum = lsum * alpha + ps;
 #pragma unroll
-      for (int db = 0; db < D / 32; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-#pragma unroll
       for (int db = 0; db < D / 32; ++db) {
         bf16x8 vfr[4];
 #pragma unroll
@@ -177,7 +189,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
         for (int kk = 0; kk < 4; ++kk) oacc[db] = mfma32(vfr[kk], pf[kk], oacc[db]);
       }
     }
-    if (t + 1 < ntiles) swrite((t + 1) & 1);
     __syncthreads();
   }
 
