@@ -125,3 +125,23 @@ def test_deterministic_training_steps_are_bitwise_reproducible(monkeypatch):
     assert runs[0][0] == runs[1][0]
     assert torch.equal(runs[0][1], runs[1][1])
     assert torch.equal(runs[0][2], runs[1][2])
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+def test_forward_deferred_rescale_growing_scores(D, causal):
+    """The forward keeps a stale row max until a tile raises it by more than 2^8
+    (csrc/attention.hip): scores that grow along the keys (small steps, deferred) with
+    occasional spikes (large steps, rescaled) against the fp32 reference."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    B, T, H = 1, 1024, 2
+    q = torch.randn(B, T, H, D, device=DEV, generator=g)
+    k = torch.randn(B, T, H, D, device=DEV, generator=g)
+    ramp = 0.2 + 2.5 * torch.arange(T, device=DEV).float() / T
+    k = k * ramp.view(1, T, 1, 1)
+    k[:, ::97] *= 6.0
+    v = torch.randn(B, T, H, D, device=DEV, generator=g)
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    o, _ = _C().attn_fwd(q, k, v, causal, 1.0 / math.sqrt(D))
+    want = ref.attention(q.float(), k.float(), v.float(), causal)
+    assert rel_err(o, want) < 3e-2
