@@ -366,13 +366,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 
 using namespace orion;
 
-// ORION_GEMM_CFG: 7 = phase-interleaved kernel (csrc/gemm_phased.hip, default), 0 = BK 64 x 2 stages, 1 = ping-pong, 2 = BK 32 x 4-stage ring,
+// ORION_GEMM_CFG: 7 = phase-interleaved kernel (csrc/gemm_phased.hip, default; 8 = its 4-quadrant
+// schedule), 0 = BK 64 x 2 stages, 1 = ping-pong, 2 = BK 32 x 4-stage ring,
 // 3 = BK 32 x 5-stage ring (160 KB: three stages in flight), 4/5/6 = 4 waves of 128 x 128
 // with BK 64 x 2 / BK 32 x 4 / BK 32 x 5 (docs/PERFORMANCE.md, "In-tree GEMM study").
 static int gemm_cfg() {  // read per call: microbenchmarks switch variants in one process
   const char* e = getenv("ORION_GEMM_CFG");
   const int c = e ? atoi(e) : 7;
-  return c < 0 || c > 7 ? 7 : c;
+  return c < 0 || c > 8 ? 7 : c;
 }
 
 template <bool WKM, int EPI, int BK, int NS, int WM = 4>
@@ -436,7 +437,9 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
              M, N, K, (N + 255) / 256, 0};
   if (const char* e = getenv("ORION_GEMM_DIAG")) a.flags = atoi(e);
   if ((a.flags & 4) && epi == EPI_STORE) a.slabs = (float*)pre;  // slot stamps (diagnostic)
-  if (gemm_cfg() == 7 && gemm_phased_ok(a, wkm)) return gemm_phased(a, wkm, epi, st);
+  const int cfg = gemm_cfg();
+  if (cfg == 8) a.flags |= 16;  // phased kernel, SCHED 0 (8-MFMA quadrant phases)
+  if ((cfg == 7 || cfg == 8) && gemm_phased_ok(a, wkm)) return gemm_phased(a, wkm, epi, st);
   switch (epi * 2 + (wkm ? 1 : 0)) {
     case EPI_STORE * 2 + 0: return gemm_launch<false, EPI_STORE>(a, st);
     case EPI_STORE * 2 + 1: return gemm_launch<true, EPI_STORE>(a, st);

@@ -18,7 +18,8 @@ struct GemmArgs {
   const bf16_t* pre; long ldp;  // pre-activation a, [M][N] (EPI_GELU_BWD)
   int M, N, K, tiles_n;
   int flags;  // diagnostics (ORION_GEMM_DIAG): 1 = no LDS-DMA after the first stage; 2 = DMA spread over
-              // k steps (csrc/gemm.hip only); 8 = no C stores
+              // k steps (csrc/gemm.hip only); 8 = no C stores;
+              // 16 = gemm_phased.hip's 4-quadrant schedule (ORION_GEMM_CFG / ORION_WGRAD_CFG = 8)
   // split-K (EPI_WGRAD, csrc/gemm_phased.hip): work item = (k chunk of kchunk rows, tile)
   int kchunk, ksplit;
   float* slabs;          // ksplit > 1: fp32 partial tiles [ksplit][M][N]

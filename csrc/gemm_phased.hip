@@ -43,7 +43,9 @@ namespace orion {
 namespace {
 
 constexpr int PH_BK = 64, PH_IMG = 256 * PH_BK, PH_STAGE = 2 * PH_IMG;
-constexpr int PH_LDS_BYTES = 2 * PH_STAGE * 2;  // 128 KB
+constexpr int PH_LDS_BYTES = 2 * PH_STAGE * 2;  // 128 KB (SCHED 0)
+constexpr int PH2_X0 = 0, PH2_W0 = 3 * PH_IMG;   // SCHED 1: X images x3, then W images x2
+constexpr int PH2_LDS_BYTES = 5 * PH_IMG * 2;    // 160 KB
 
 ORION_DEVICE void ph_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -66,7 +68,12 @@ ORION_DEVICE void ph_wait_lds(bf16x8 (&x)[4]) {
 // STAMPS (diagnostic instantiation, ORION_GEMM_DIAG=4 with a stamp buffer, EPI_STORE only):
 // workgroup 0 records s_memtime per wave at each slot boundary into g.slabs as u64
 // [wave][1024] (scripts/gemm_stamps.py); no effect on results.
-template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
+// SCHED 0 (flags & 16: ORION_GEMM_CFG / ORION_WGRAD_CFG = 8): four 8-MFMA quadrant phases per
+// k-tile (2-deep ring of 64 KB stages).
+// SCHED 1 (default, 2-3 % faster): two 16-MFMA phases per k-tile (n-half 0, n-half 1: half the barriers); the X
+// images are triple-buffered (3 x 32 KB) so that both X pieces, read in the first phase, can
+// be staged two phases earlier than the W pieces; W double-buffered (2 x 32 KB): 160 KB.
+template <bool XKM, bool WKM, int EPI, bool STAMPS = false, int SCHED = 0>
 __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -150,20 +157,29 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
           const int kr0 = b * 8, kr = kr0 + lr;
           const int col = n0 + grp * 128 + hh * 64 + 8 * (slot ^ swz<64>(kr));
           vo[p][e] = (unsigned)(((long)kr * g.ldw + min(col, g.N - 8)) * 2);
-          ld[p][e] = PH_IMG + (2 * grp + hh) * 4096 + kr0 * 64;
+          ld[p][e] = (2 * grp + hh) * 4096 + kr0 * 64;
         } else {
           const int row0 = grp * 128 + hh * 64 + b * 8, row = row0 + lr;
           const int ch = slot ^ swz<64>(row);
           vo[p][e] = (unsigned)(((long)min(n0 + row, g.N - 1) * g.ldw + 8 * ch) * 2);
-          ld[p][e] = PH_IMG + row0 * 64;
+          ld[p][e] = row0 * 64;
         }
       }
     }
   };
   set_tile(m0, n0, kc);
+  // LDS images of k-tile t
+  auto ximg = [&](int t) -> bf16_t* {
+    if constexpr (SCHED == 1) return smem + PH2_X0 + (t % 3) * PH_IMG;
+    else return smem + (t & 1) * PH_STAGE;
+  };
+  auto wimg = [&](int t) -> bf16_t* {
+    if constexpr (SCHED == 1) return smem + PH2_W0 + (t & 1) * PH_IMG;
+    else return smem + (t & 1) * PH_STAGE + PH_IMG;
+  };
   auto issue = [&](int p, int t) {
-    bf16_t* base = smem + (t & 1) * PH_STAGE;
     const bool isx = p == 1 || p == 2;
+    bf16_t* base = isx ? ximg(t) : wimg(t);
     const unsigned so = (unsigned)t * (isx ? xstep : wstep);
     ORION_DASSERT(t < nk);
 #pragma unroll
@@ -216,8 +232,8 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   auto phase = [&](auto Qc, auto ISSUEc, auto VMNc, int t) {
     constexpr int Q = decltype(Qc)::value, VMN = decltype(VMNc)::value;
     constexpr bool ISSUE = decltype(ISSUEc)::value;
-    const bf16_t* Xs = smem + (t & 1) * PH_STAGE;
-    const bf16_t* Ws = Xs + PH_IMG;
+    const bf16_t* Xs = ximg(t);
+    const bf16_t* Ws = wimg(t);
     // ---- READ slot
     stamp();  // R: slot start (after the barrier)
     if constexpr (Q == 0) {
@@ -263,6 +279,54 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
     stamp();  // E: MFMAs issued
     ph_barrier();
   };
+  // SCHED 1: phase H of k-tile t: READ slot = this phase's fragments (H 0: W n-half 0 and all
+  // of X, 16; H 1: W n-half 1, 8) + its pieces (H 0: A(t+1), B(t+2); H 1: D(t+1), C(t+2)),
+  // then VMN loads left in flight (this phase's: every older one has landed, and each piece
+  // is read >= 2 phases after it was issued); MMA slot = 16 MFMAs on 4 accumulators per step.
+  // X registers are rewritten one MMA slot after their last use: an MFMA has read its A/B
+  // operands once issued, and every MFMA of the slot is issued before its closing barrier.
+  auto phase2 = [&](auto Hc, auto ISWc, auto ISXc, auto VMNc, int t) {
+    constexpr int H = decltype(Hc)::value, VMN = decltype(VMNc)::value;
+    constexpr bool ISW = decltype(ISWc)::value, ISX = decltype(ISXc)::value;
+    const bf16_t* Xs = ximg(t);
+    const bf16_t* Ws = wimg(t);
+    stamp();
+    if constexpr (H == 0) {
+      read_w(W0[0], Ws, 0, 0);
+      read_w(W0[1], Ws, 0, 1);
+      read_x(X0, Xs, 0);
+      read_x(X1, Xs, 1);
+      if constexpr (ISW) issue(0, t + 1);
+      if constexpr (ISX) issue(1, t + 2);
+    } else {
+      read_w(W1[0], Ws, 1, 0);
+      read_w(W1[1], Ws, 1, 1);
+      if constexpr (ISW) issue(3, t + 1);
+      if constexpr (ISX) issue(2, t + 2);
+    }
+    wait_vm_exact<VMN>();
+    ph_barrier();
+    if constexpr (H == 0) {
+      ph_wait_lds(W0[0], X0);
+      ph_wait_lds(W0[1], X1);
+    } else {
+      ph_wait_lds(W1[0], W1[1]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    stamp();
+    bf16x8 (&w)[2][4] = H == 0 ? W0 : W1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc[2 * H + i][0] = mfma32(w[i][s], X0[s], acc[2 * H + i][0]);
+        acc[2 * H + i][1] = mfma32(w[i][s], X1[s], acc[2 * H + i][1]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    stamp();
+    ph_barrier();
+  };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
@@ -275,13 +339,24 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
 
   // prologue: the pieces of phases -6 .. -1 (A0 B0 C0 D0 A1 B1); phase 0 needs A0 and B0
   auto prologue = [&] {
-    issue(0, 0);
-    issue(1, 0);
-    issue(2, 0);
-    issue(3, 0);
-    if (nk > 1) {
-      issue(0, 1);
-      issue(1, 1);
+    if constexpr (SCHED == 1) {  // B0 C0 A0 D0 B1 C1: phase 0 needs the first three
+      issue(1, 0);
+      issue(2, 0);
+      issue(0, 0);
+      issue(3, 0);
+      if (nk > 1) {
+        issue(1, 1);
+        issue(2, 1);
+      }
+    } else {
+      issue(0, 0);
+      issue(1, 0);
+      issue(2, 0);
+      issue(3, 0);
+      if (nk > 1) {
+        issue(0, 1);
+        issue(1, 1);
+      }
     }
   };
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(g.out, (unsigned)((long)g.M * g.ldo * 2));
@@ -295,12 +370,13 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   while (true) {
     // A0 and B0 landed: 8 later prologue loads (4 if nk = 1) may be in flight, plus the
     // previous tile's STORES epilogue stores issued after them (vmcnt retires in order)
+    constexpr int PRO_LATE = SCHED == 1 ? 6 : 8;  // prologue loads after the first phase's
     if (first || EPI == EPI_WGRAD) {  // (EPI_WGRAD's stores are not counted: wait for them)
-      if (nk > 1) wait_vm_exact<8>();
-      else wait_vm_exact<4>();
+      if (nk > 1) wait_vm_exact<PRO_LATE>();
+      else wait_vm_exact<PRO_LATE - 4>();
     } else {
-      if (nk > 1) wait_vm_exact<8 + STORES>();
-      else wait_vm_exact<4 + STORES>();
+      if (nk > 1) wait_vm_exact<PRO_LATE + STORES>();
+      else wait_vm_exact<PRO_LATE - 4 + STORES>();
     }
     first = false;
 #pragma unroll
@@ -313,6 +389,19 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
     // piece issues run through phase 4 nk - 7; after phase P a wave leaves the loads of
     // phases P-3 .. P in flight (8 while every phase issues, fewer in the tail)
     int t = 0;
+    if constexpr (SCHED == 1) {
+      for (; t < nk - 2; ++t) {
+        phase2(I0(), Y(), Y(), I4(), t);
+        phase2(I1(), Y(), Y(), I4(), t);
+      }
+      if (nk >= 2) {  // t = nk - 2: A, D of k-tile nk - 1
+        phase2(I0(), Y(), N(), I2(), t);
+        phase2(I1(), Y(), N(), I2(), t);
+        ++t;
+      }
+      phase2(I0(), N(), N(), I0(), t);
+      phase2(I1(), N(), N(), I0(), t);
+    } else {
     for (; t < nk - 2; ++t) {
       phase(I0(), Y(), I8(), t);
       phase(I1(), Y(), I8(), t);
@@ -330,6 +419,7 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
     phase(I1(), N(), I0(), t);
     phase(I2(), N(), I0(), t);
     phase(I3(), N(), I0(), t);
+    }
     if (grp == 0) ph_barrier();  // match group 1's barrier count: every LDS read is done
 
     // next tile's prologue DMA first, then this tile's epilogue: the loads land while the
@@ -414,12 +504,13 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
   }
 }
 
-template <bool XKM, bool WKM, int EPI, bool STAMPS>
+template <bool XKM, bool WKM, int EPI, bool STAMPS, int SCHED>
 static int gemm_phased_launch_s(const GemmArgs& a, hipStream_t st) {
+  constexpr int lds = SCHED == 1 ? PH2_LDS_BYTES : PH_LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_phased_kernel<XKM, WKM, EPI, STAMPS>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, PH_LDS_BYTES) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)gemm_phased_kernel<XKM, WKM, EPI, STAMPS, SCHED>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
       return -5;
     attr = true;
   }
@@ -433,16 +524,20 @@ static int gemm_phased_launch_s(const GemmArgs& a, hipStream_t st) {
   }
   const long work = (long)((a.M + 255) / 256) * a.tiles_n * a.ksplit;
   const int grid = (int)(work < ncu ? work : ncu);
-  gemm_phased_kernel<XKM, WKM, EPI, STAMPS><<<grid, 512, PH_LDS_BYTES, st>>>(a);
+  gemm_phased_kernel<XKM, WKM, EPI, STAMPS, SCHED><<<grid, 512, lds, st>>>(a);
   return (int)hipGetLastError();
 }
 
 template <bool XKM, bool WKM, int EPI>
 static int gemm_phased_launch(const GemmArgs& a, hipStream_t st) {
   if constexpr (!XKM && EPI == EPI_STORE) {
-    if ((a.flags & 4) && a.slabs) return gemm_phased_launch_s<XKM, WKM, EPI, true>(a, st);
+    if ((a.flags & 4) && a.slabs) {
+      if (a.flags & 16) return gemm_phased_launch_s<XKM, WKM, EPI, true, 0>(a, st);
+      return gemm_phased_launch_s<XKM, WKM, EPI, true, 1>(a, st);
+    }
   }
-  return gemm_phased_launch_s<XKM, WKM, EPI, false>(a, st);
+  if (a.flags & 16) return gemm_phased_launch_s<XKM, WKM, EPI, false, 0>(a, st);
+  return gemm_phased_launch_s<XKM, WKM, EPI, false, 1>(a, st);
 }
 
 // Requirements beyond orion_gemm's: every operand and output byte offset fits in 32 bits

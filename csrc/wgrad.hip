@@ -188,8 +188,8 @@ constexpr int WG_PHASED = 7;
 static int wg_cfg(int M) {
   const char* e = getenv("ORION_WGRAD_CFG");
   int c = e ? atoi(e) : WG_PHASED;
-  if (!(c == WG_PHASED || (c >= 0 && c < WG_NCFG))) c = WG_PHASED;
-  return c == WG_PHASED && M % 64 ? 0 : c;
+  if (!(c == WG_PHASED || c == WG_PHASED + 1 || (c >= 0 && c < WG_NCFG))) c = WG_PHASED;
+  return c >= WG_PHASED && M % 64 ? 0 : c;
 }
 
 }  // namespace orion
@@ -198,7 +198,7 @@ using namespace orion;
 
 static int wg_bk(int M) {
   const int c = wg_cfg(M);
-  return c == WG_PHASED ? 64 : 16 * WG_CFGS[c].ks;
+  return c >= WG_PHASED ? 64 : 16 * WG_CFGS[c].ks;
 }
 
 // Split count: minimise (rounds of one-workgroup-per-CU) x (rows per workgroup) plus
@@ -234,7 +234,7 @@ int orion_wgrad_effective_splits(int M, int S) {
 }
 
 static int wgrad_lds(int M) {
-  if (wg_cfg(M) == WG_PHASED) return 128 * 1024;
+  if (wg_cfg(M) >= WG_PHASED) return 160 * 1024;
   const WgCfg c = WG_CFGS[wg_cfg(M)];
   return c.ns * c.ks * 16 * 128 * 4 * (int)sizeof(bf16_t);
 }
@@ -254,8 +254,9 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   if (S > 1 && !slabs) return -4;
   const int t1 = (N1 + 255) / 256, t2 = (N2 + 255) / 256;
   const int ntiles = t1 * t2;
-  if (wg_cfg(M) == WG_PHASED) {
+  if (wg_cfg(M) >= WG_PHASED) {
     GemmArgs a{};
+    a.flags = wg_cfg(M) == WG_PHASED + 1 ? 16 : 0;  // ORION_WGRAD_CFG=8: the 4-quadrant schedule
     a.X = (const bf16_t*)A;  // [M tokens][N1]: the k-major "X" operand, rows of out = N1
     a.ldx = lda;
     a.W = (const bf16_t*)B;  // [M tokens][N2]

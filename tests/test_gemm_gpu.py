@@ -83,9 +83,11 @@ def test_gemm_batched_input_shape_and_strided_rows():
 
 @pytest.mark.parametrize("M,N,K", [(300, 264, 128), (1000, 768, 768), (777, 50304, 128)])
 @pytest.mark.parametrize("wkm", [False, True])
-def test_gemm_two_stage_kernel(M, N, K, wkm, monkeypatch):
-    """csrc/gemm.hip's 2-stage kernel (ORION_GEMM_CFG=0, read per call)."""
-    monkeypatch.setenv("ORION_GEMM_CFG", "0")
+@pytest.mark.parametrize("cfg", ["0", "8"])
+def test_gemm_other_schedules(M, N, K, wkm, cfg, monkeypatch):
+    """csrc/gemm.hip's 2-stage kernel (ORION_GEMM_CFG=0) and the phased kernel's 4-quadrant
+    schedule (8); the variable is read per call."""
+    monkeypatch.setenv("ORION_GEMM_CFG", cfg)
     g = torch.Generator(device=DEV).manual_seed(M + 3 * N + K)
     x = _rnd(g, M, K)
     w = _rnd(g, K, N) if wkm else _rnd(g, N, K)
@@ -94,7 +96,7 @@ def test_gemm_two_stage_kernel(M, N, K, wkm, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768), (8224, 200, 264)])
-@pytest.mark.parametrize("cfg", ["7", "0"])
+@pytest.mark.parametrize("cfg", ["7", "8", "0"])
 @pytest.mark.parametrize("acc", [False, True])
 def test_wgrad_phased_and_two_stage_into_fp32(M, N1, N2, cfg, acc, monkeypatch):
     """Weight gradients on the phased kernel (split-K work items, fp32 slabs) and on
