@@ -29,13 +29,17 @@ from ._ext import C
 from .determinism import deterministic
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
-# Linear-layer forward (x W^T [+ b]) and input gradient (dy W) run on hipBLASLt by default
-# (csrc/gemm.hip measures 0.75-1.05 PF/s against hipBLASLt's 0.9-1.4 on the GPT-2 shapes:
-# docs/PERFORMANCE.md).  The in-tree kernel is used when ORION_GEMM=hip, and always inside
-# a HIP-graph capture (``hip_gemms()``): its arguments are plain kernel arguments captured
-# in the graph node, with no library-side host state between replays -- and in the
+# Linear-layer forward (x W^T [+ b]) and input gradient (dy W).  ORION_GEMM=blas (default):
+# hipBLASLt.  ORION_GEMM=auto: the in-tree phased kernel (csrc/gemm_phased.hip) for the input
+# gradients it wins in isolation -- narrow outputs (N <= 1024) over K <= 8192 with >= 256
+# output tiles: the GPT-2 qkv / attn-proj / fc dgrads run 5-18 % faster than hipBLASLt
+# (profiles/gemm_study/bench_sched1_vs_blas_gpt2.log) -- but the whole GPT-2 step measured
+# 996.6k vs 1000.1k tok/s (3 alternating runs each), so it is not the default; hipBLASLt
+# keeps the forward shapes, the LM head and Llama-7B's wide shapes (1-35 % faster there).
+# ORION_GEMM=hip routes every eligible GEMM in-tree.  Inside a HIP-graph capture (``hip_gemms()``)
+# every eligible GEMM is in-tree (no library-side host state between replays), and so in the
 # deterministic mode (ops/determinism.py): one workgroup per output tile, no split-K.
-_GEMM_IMPL = os.environ.get("ORION_GEMM", "blas")  # "blas" | "hip"
+_GEMM_IMPL = os.environ.get("ORION_GEMM", "blas")  # "blas" | "auto" | "hip"
 _FORCE_HIP = 0
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD = 0, 1, 2, 3
@@ -52,15 +56,30 @@ def hip_gemms():
         _FORCE_HIP -= 1
 
 
-def use_hip_gemm(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
-    if not (_FORCE_HIP or _GEMM_IMPL == "hip" or deterministic()):
-        return False
+def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
     K = x.shape[-1]
     N = w.shape[1] if w_kmajor else w.shape[0]
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and K % 64 == 0 and N % 8 == 0 and w.is_contiguous() and x.stride(-1) == 1
             and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
             and (x.dim() == 2 and x.stride(0) % 8 == 0 or x.is_contiguous()))
+
+
+def _hip_wins(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
+    if not w_kmajor:
+        return False
+    K, N = x.shape[-1], w.shape[1]
+    M = x.numel() // K
+    return N <= 1024 and K <= 8192 and M * N >= 256 * 256 * 256
+
+
+def use_hip_gemm(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
+    if _GEMM_IMPL == "blas" and not (_FORCE_HIP or deterministic()):
+        return False
+    forced = _FORCE_HIP or _GEMM_IMPL == "hip" or deterministic()
+    if not forced and not (_GEMM_IMPL == "auto" and _hip_wins(x, w, w_kmajor)):
+        return False
+    return _hip_eligible(x, w, w_kmajor)
 
 
 def linear_fwd(x, w, b=None):
