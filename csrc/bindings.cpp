@@ -52,7 +52,9 @@ int orion_attn_bwd(const orion::AttnParams&, int, bool, float*, hipStream_t);
 int orion_attn_dq_convert(const float*, void*, long, long, long, int, int, int, int, hipStream_t);
 int orion_attn_bwd_split(const orion::AttnParams&, int, bool, float*, hipStream_t);
 int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, void*, long,
-               const void*, void*, long, const void*, long, hipStream_t);
+               const void*, void*, long, const void*, long, hipStream_t, void* db = nullptr,
+               int db_f32 = 0, float* part = nullptr);
+int orion_gemm_colsum_scratch(int M, int N);
 
 namespace {
 
@@ -424,6 +426,46 @@ std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor,
   return {out, out2};
 }
 
+// da = (dy . w) * GELU'(pre + bias) (w (K, N) k-major: the MLP output projection's weight
+// (C, F) read as the input gradient's operand) and db = colsum(da), the fused backward of
+// gelu(pre + bias) -> linear: csrc/gemm_phased.hip's EPI_GELU_BWD epilogue with per-64-row
+// column-sum partials.  db goes into db_out (an fp32/bf16 gradient-arena slice) when given.
+std::tuple<Tensor, Tensor> gemm_gelu_bwd(const Tensor& dy, const Tensor& w, const Tensor& pre,
+                                         const c10::optional<Tensor>& bias,
+                                         const c10::optional<Tensor>& db_out) {
+  check_bf16(dy, "dy");
+  check_bf16(w, "w");
+  check_bf16(pre, "pre");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemm_gelu_bwd: w must be a contiguous (K, N)");
+  const int64_t K = w.size(0), N = w.size(1);
+  TORCH_CHECK(dy.size(-1) == K, "gemm_gelu_bwd: dy (..., K)");
+  auto x2 = dy.reshape({-1, K});
+  TORCH_CHECK(x2.stride(1) == 1, "gemm_gelu_bwd: dy must flatten to rows");
+  const int64_t M = x2.size(0);
+  TORCH_CHECK(M < (1LL << 31) && N < (1 << 30), "gemm_gelu_bwd: shape too large");
+  auto pc = pre.reshape({-1, N});
+  TORCH_CHECK(pc.size(0) == M && pc.stride(1) == 1, "gemm_gelu_bwd: pre must be (M, N)");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  Tensor bc;
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_bf16(*bias, "bias");
+    bc = bias->contiguous();
+    TORCH_CHECK(bc.numel() == N, "gemm_gelu_bwd: bias must have N elements");
+    bp = bc.data_ptr();
+  }
+  auto sizes = pre.sizes().vec();
+  auto out = at::empty({M, N}, dy.options());
+  const bool given = has_out(db_out, N, "db_out");
+  auto db = given ? *db_out : at::empty({N}, bias.has_value() && bias->defined() ? bias->options() : dy.options());
+  auto part = at::empty({(long)orion_gemm_colsum_scratch((int)M, (int)N)}, dy.options().dtype(at::kFloat));
+  check_launch(orion_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), (int)M, (int)N,
+                          (int)K, 1, 3, out.data_ptr(), N, bp, nullptr, 0, pc.data_ptr(), pc.stride(0),
+                          cur_stream(), db.data_ptr(), is_f32(db) ? 1 : 0, part.data_ptr<float>()),
+               "gemm_gelu_bwd");
+  return {out.view(sizes), given ? Tensor() : db};
+}
+
 // ------------------------------------------------------------------ optimizer
 void grad_sumsq(const Tensor& g, Tensor out) {
   check_grad_out(g, "grads");
@@ -674,6 +716,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("wgrad_splits(int M, int N1, int N2) -> int", &wgrad_splits);  // host-only helper
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
+  m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
@@ -700,6 +743,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("wgrad_into", &wgrad_into);
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
   m.impl("gemm", &gemm);
+  m.impl("gemm_gelu_bwd", &gemm_gelu_bwd);
   m.impl("grad_sumsq", &grad_sumsq);
   m.impl("adamw_flat", &adamw_flat);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);

@@ -422,9 +422,19 @@ static int gemm_launch(const GemmArgs& a, hipStream_t st) {
 // out[M][N] = X[M][K] . op(W) with op(W) = W^T for W [N][K] (wkm = 0) or W for W [K][N]
 // (wkm = 1), epilogue `epi` (GemmEpi).  Requirements (else -1): K % 64 == 0, N % 8 == 0,
 // N >= 8, 8-element aligned leading dims, 16-byte aligned base pointers.
+int orion_colsum_bf16(const void* m, void* out, float* part, int rows, int C, int out_f32,
+                      hipStream_t st);
+int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, int f32,
+                           hipStream_t st);
+
+// EPI_GELU_BWD with db: db[N] (fp32 when db_f32, else bf16) = column sums of the result (the
+// bias gradient) through part (orion_gemm_colsum_scratch(M, N) floats): per-64-row partials
+// from the phased kernel's epilogue, else a column-sum pass over out.
+int orion_gemm_colsum_scratch(int M, int N) { return ((M + 63) / 64 + 32) * N; }
+
 int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, int wkm,
                int epi, void* out, long ldo, const void* bias, void* out2, long ldo2,
-               const void* pre, long ldp, hipStream_t st) {
+               const void* pre, long ldp, hipStream_t st, void* db, int db_f32, float* part) {
   if (M < 1 || K < 64 || K % 64 || N % 8 || N < 8) return -1;
   if ((ldx | ldw | ldo) % 8) return -1;
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
@@ -432,6 +442,7 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   if ((epi == EPI_BIAS || epi == EPI_BIAS_GELU) && !bias) return -3;
   if (epi == EPI_BIAS_GELU && (!out2 || ldo2 % 8 || (reinterpret_cast<uintptr_t>(out2) & 15))) return -3;
   if (epi == EPI_GELU_BWD && (!pre || ldp % 4)) return -3;
+  if (db && (epi != EPI_GELU_BWD || !part || ldo != N)) return -3;
   GemmArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)out, ldo,
              (const bf16_t*)bias, (bf16_t*)out2, ldo2, (const bf16_t*)pre, ldp,
              M, N, K, (N + 255) / 256, 0};
@@ -439,13 +450,22 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   if ((a.flags & 4) && epi == EPI_STORE) a.slabs = (float*)pre;  // slot stamps (diagnostic)
   const int cfg = gemm_cfg();
   if (cfg == 8) a.flags |= 16;  // phased kernel, SCHED 0 (8-MFMA quadrant phases)
-  if ((cfg == 7 || cfg == 8) && gemm_phased_ok(a, wkm)) return gemm_phased(a, wkm, epi, st);
+  int rc;
+  if ((cfg == 7 || cfg == 8) && gemm_phased_ok(a, wkm)) {
+    const int rows = (M + 63) / 64;
+    if (db) a.colsum = part;
+    rc = gemm_phased(a, wkm, epi, st);
+    if (rc == 0 && db) rc = orion_colsum_partials2(part, part + (long)rows * N, db, rows, N, db_f32, st);
+    return rc;
+  }
   switch (epi * 2 + (wkm ? 1 : 0)) {
-    case EPI_STORE * 2 + 0: return gemm_launch<false, EPI_STORE>(a, st);
-    case EPI_STORE * 2 + 1: return gemm_launch<true, EPI_STORE>(a, st);
-    case EPI_BIAS * 2 + 0: return gemm_launch<false, EPI_BIAS>(a, st);
-    case EPI_BIAS_GELU * 2 + 0: return gemm_launch<false, EPI_BIAS_GELU>(a, st);
-    case EPI_GELU_BWD * 2 + 1: return gemm_launch<true, EPI_GELU_BWD>(a, st);
+    case EPI_STORE * 2 + 0: rc = gemm_launch<false, EPI_STORE>(a, st); break;
+    case EPI_STORE * 2 + 1: rc = gemm_launch<true, EPI_STORE>(a, st); break;
+    case EPI_BIAS * 2 + 0: rc = gemm_launch<false, EPI_BIAS>(a, st); break;
+    case EPI_BIAS_GELU * 2 + 0: rc = gemm_launch<false, EPI_BIAS_GELU>(a, st); break;
+    case EPI_GELU_BWD * 2 + 1: rc = gemm_launch<true, EPI_GELU_BWD>(a, st); break;
     default: return -4;
   }
+  if (rc == 0 && db) rc = orion_colsum_bf16(out, db, part, M, N, db_f32, st);
+  return rc;
 }

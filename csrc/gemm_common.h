@@ -25,15 +25,19 @@ struct GemmArgs {
   float* slabs;          // ksplit > 1: fp32 partial tiles [ksplit][M][N]
   const float* scale;    // ksplit == 1: out (fp32 when out_f32, else bf16) = acc * *scale
   int accumulate, out_f32;  //            (+ the value already in out when accumulate)
+  // EPI_GELU_BWD (csrc/gemm_phased.hip): fp32 column sums of the result (the bias gradient)
+  // per 64-row block, colsum[ceil(M / 64)][N]; null = none
+  float* colsum;
 };
 
 // Epilogue math of one 32 x 32 accumulator of C^T (rows n = nb + (r&3) + 8(r>>2) + 4 h32,
 // column = the lane's output row m, clamped to mc): fp32 bias / GELU / GELU-backward, one bf16
 // rounding, packed pairs pk[g4][0..1] = columns nb + 8 g4 + 4 h32 + 0..3.  GELU2 = 1: the
-// second output of EPI_BIAS_GELU (gelu(a)) instead of the first (a).
+// second output of EPI_BIAS_GELU (gelu(a)) instead of the first (a).  EPI_GELU_BWD multiplies by
+// GELU'(pre + bias) (bias optional).  vals (if given): the 16 fp32 values before rounding.
 template <int EPI, bool GELU2 = false>
 ORION_DEVICE void gemm_epi_values(const GemmArgs& g, const f32x16& acc, int mc, int nb, int h32,
-                                  unsigned (&pk)[4][2]) {
+                                  unsigned (&pk)[4][2], float* vals = nullptr) {
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
     const int n = nb + 8 * g4 + 4 * h32;
@@ -49,12 +53,24 @@ ORION_DEVICE void gemm_epi_values(const GemmArgs& g, const f32x16& acc, int mc, 
     if constexpr (EPI == EPI_GELU_BWD) {
       ORION_DASSERT(mc < g.M && nc + 4 <= g.N);
       const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(g.pre + (long)mc * g.ldp + nc);
+      float pb[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= gelu_tanh_grad_f(bf2f(a4[e]));
+      for (int e = 0; e < 4; ++e) pb[e] = bf2f(a4[e]);
+      if (g.bias) {
+        const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + nc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pb[e] += bf2f(b4[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= gelu_tanh_grad_f(pb[e]);
     }
     if constexpr (GELU2) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = gelu_tanh_f(v[e]);
+    }
+    if (vals) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vals[4 * g4 + e] = v[e];
     }
     pk[g4][0] = pack_bf16x2(v[0], v[1]);
     pk[g4][1] = pack_bf16x2(v[2], v[3]);

@@ -470,13 +470,16 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
       if (!more) break;
       continue;
     }
+    constexpr bool CS = EPI == EPI_GELU_BWD;  // column sums of the result (bias gradient)
+    const int mb = cm0 + wm * 64;              // this wave's 64-row block
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m = cm0 + wm * 64 + j * 32 + l32;
-      const int mc = min(m, g.M - 1);
+    for (int i = 0; i < 4; ++i) {
+      const int nb = cn0 + grp * 128 + i * 32;
+      float cs[CS ? 16 : 1];  // register r of acc[i][.]: this lane's sum over j
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int nb = cn0 + grp * 128 + i * 32;
+      for (int j = 0; j < 2; ++j) {
+        const int m = mb + j * 32 + l32;
+        const int mc = min(m, g.M - 1);
         auto put = [&](const unsigned (&pk)[4][2], __amdgpu_buffer_rsrc_t r, long ld) {
 #pragma unroll
           for (int pr = 0; pr < 2; ++pr) {
@@ -492,11 +495,45 @@ __global__ __launch_bounds__(512, 1) void gemm_phased_kernel(GemmArgs g) {
           }
         };
         unsigned pk[4][2];
-        gemm_epi_values<EPI>(g, acc[i][j], mc, nb, h32, pk);
+        if constexpr (CS) {
+          float v[16];
+          gemm_epi_values<EPI>(g, acc[i][j], mc, nb, h32, pk, v);
+          const float keep = m < g.M ? 1.f : 0.f;  // rows past M repeat row M - 1
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cs[r] = j ? cs[r] + keep * v[r] : keep * v[r];
+        } else {
+          gemm_epi_values<EPI>(g, acc[i][j], mc, nb, h32, pk);
+        }
         put(pk, ro, g.ldo);
         if constexpr (EPI == EPI_BIAS_GELU) {
           gemm_epi_values<EPI, true>(g, acc[i][j], mc, nb, h32, pk);
           put(pk, ro2, g.ldo2);
+        }
+      }
+      if constexpr (CS) {
+        if (g.colsum) {
+          // sum over the 32 lanes of each half (same columns n, rows m = lane): four halving
+          // exchange steps (at offset o a lane keeps the half of its live values selected by
+          // lane bit o and adds its partner's copy of it), then one full add with lane ^ 1;
+          // lane l32 ends with register r = l32 / 2
+          auto step = [&](auto Oc) {
+            constexpr int o = decltype(Oc)::value, half = o / 2;
+            const bool up = (l32 & o) != 0;
+#pragma unroll
+            for (int k = 0; k < half; ++k) {
+              const float send = up ? cs[k] : cs[half + k];
+              const float keep = up ? cs[half + k] : cs[k];
+              cs[k] = keep + __shfl_xor(send, o);
+            }
+          };
+          step(std::integral_constant<int, 16>());
+          step(std::integral_constant<int, 8>());
+          step(std::integral_constant<int, 4>());
+          step(std::integral_constant<int, 2>());
+          const float tot = cs[0] + __shfl_xor(cs[0], 1);
+          const int r = l32 >> 1;
+          const int n = nb + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          if (!(l32 & 1) && mb < g.M && n < g.N) g.colsum[(long)(mb / 64) * g.N + n] = tot;
         }
       }
     }

@@ -91,11 +91,8 @@ class MLP(nn.Module):
         self.dropout = cfg.dropout
 
     def forward(self, x, fuse_out_bias=False):
-        if self.c_fc.bias is not None:
-            h = ops.bias_gelu(ops.linear(x, self.c_fc.weight), self.c_fc.bias)
-        else:
-            h = ops.gelu(ops.linear(x, self.c_fc.weight))
-        y = ops.linear(h, self.c_proj.weight, None if fuse_out_bias else self.c_proj.bias)
+        y = ops.gelu_linear(ops.linear(x, self.c_fc.weight), self.c_fc.bias, self.c_proj.weight,
+                            None if fuse_out_bias else self.c_proj.bias)
         if self.dropout and self.training:
             y = F.dropout(y, self.dropout)
         return y

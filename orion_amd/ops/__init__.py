@@ -120,6 +120,19 @@ def bias_gelu(x, bias):
     return ref.bias_gelu(x, bias)
 
 
+def gelu_linear(a, fc_bias, weight, bias=None):
+    """linear(gelu(a + fc_bias), weight, bias): the MLP tail.  On the GPU one autograd node
+    whose backward is a single GEMM with the GELU derivative and the fc-bias gradient fused
+    into its epilogue (ops/activations.py); elsewhere bias_gelu then linear."""
+    b = _gpu(a)
+    if b == "hip":
+        from .activations import fused_mlp_ok, gelu_linear_hip
+        if fused_mlp_ok(a, weight):
+            return gelu_linear_hip(a, fc_bias, weight, bias)
+    h = gelu(a) if fc_bias is None else bias_gelu(a, fc_bias)
+    return linear(h, weight, bias)
+
+
 def swiglu(gate_up):
     """silu(gate) * up on a packed (..., 2F) [gate | up] projection -> (..., F)."""
     b = _gpu(gate_up)

@@ -58,6 +58,9 @@ def main():
               ("lmhead_fwd", "fwd", 50304, 768, 0),
               ("qkv_dgrad", "dgrad", 768, 2304, 0), ("attnproj_dgrad", "dgrad", 768, 768, 0),
               ("fc_dgrad", "dgrad", 768, 3072, 0), ("mlpproj_dgrad+gelu_bwd", "dgrad", 3072, 768, 3),
+              # 5: gemm_gelu_bwd (GELU'(pre + b) and the bias gradient in the epilogue) against
+              # the unfused dgrad GEMM + bias_gelu_bwd (which also sums the bias gradient)
+              ("mlpproj_dgrad+gelu_bwd+db", "dgrad", 3072, 768, 5),
               ("lmhead_dgrad", "dgrad", 768, 50304, 0)]
     if a.llama:
         shapes = [("l_qkv_fwd", "fwd", 12288, 4096, 0), ("l_o_fwd", "fwd", 4096, 4096, 0),
@@ -79,8 +82,8 @@ def main():
             M = a.M
         x = rnd(M, K)
         w = rnd(N, K) if kind == "fwd" else rnd(K, N)
-        b = rnd(N) if epi in (1, 2) else None
-        pre = rnd(M, N) if epi == 3 else None
+        b = rnd(N) if epi in (1, 2, 5) else None
+        pre = rnd(M, N) if epi in (3, 5) else None
         if kind == "fwd":
             hip = lambda: ops.gemm(x, w, False, epi, b, None)
             if epi == 2:
@@ -89,7 +92,10 @@ def main():
                 blas = lambda: torch.nn.functional.linear(x, w, b)
         else:
             hip = lambda: ops.gemm(x, w, True, epi, None, pre)
-            if epi == 3:
+            if epi == 5:
+                hip = lambda: ops.gemm_gelu_bwd(x, w, pre, b, None)
+                blas = lambda: ops.bias_gelu_bwd(x @ w, pre, b, None)
+            elif epi == 3:
                 # the unfused path: dgrad GEMM, then the GELU backward kernel (x = pre, no bias)
                 blas = lambda: ops.bias_gelu_bwd(x @ w, pre, None, None)
             else:
@@ -111,15 +117,17 @@ def main():
             rec[f"cfg{c}_TFs"] = round(flop / t[f"hip{c}"] / 1e9, 1)
         if a.check:
             ref = (x.float() @ (w.float().t() if kind == "fwd" else w.float()))
-            if b is not None:
+            if b is not None and epi != 5:
                 ref = ref + b.float()
             os.environ["ORION_GEMM_CFG"] = cfgs[0]
             got = hip()
             o = got[0].float()
-            if epi == 3:
+            if epi in (3, 5):
                 from orion_amd.ops import reference as R
                 gp = torch.func.grad(lambda z: R.gelu_tanh(z).sum())
-                ref = ref * gp(pre.float())
+                ref = ref * gp(pre.float() + (b.float() if epi == 5 else 0))
+                if epi == 5:
+                    rec["rel_err_db"] = float((got[1].float() - ref.sum(0)).norm() / ref.sum(0).norm())
             rec["rel_err"] = float((o - ref).norm() / ref.norm())
             if epi == 2:
                 from orion_amd.ops import reference as R

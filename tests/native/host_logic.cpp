@@ -15,7 +15,9 @@ int orion_wgrad_effective_splits(int M, int S);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
                 const float*, int, int, hipStream_t);
 int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, void*, long,
-               const void*, void*, long, const void*, long, hipStream_t);
+               const void*, void*, long, const void*, long, hipStream_t, void* db = nullptr,
+               int db_f32 = 0, float* part = nullptr);
+int orion_gemm_colsum_scratch(int M, int N);
 int orion_layernorm_bwd_blocks(int rows);
 int orion_colsum_scratch(int rows, int C);
 int orion_rmsnorm_bwd_blocks(int rows);
@@ -63,6 +65,11 @@ int main() {
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 0, 2, o, 64, p, nullptr, 64, nullptr, 0, 0) == -3);        // gelu out2 missing
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 3, o, 64, nullptr, nullptr, 0, nullptr, 0, 0) == -3);   // pre missing
   CHECK(orion_gemm(p, 64, p, 64, 0, 64, 64, 0, 0, o, 64, nullptr, nullptr, 0, nullptr, 0, 0) == -1);    // M = 0
+  float part[4096];
+  CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 0, o, 64, nullptr, nullptr, 0, nullptr, 0, 0, o, 0, part) == -3);  // db needs epi 3
+  CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 3, o, 64, nullptr, nullptr, 0, p, 64, 0, o, 0, nullptr) == -3);  // db needs scratch
+  CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 3, o, 72, nullptr, nullptr, 0, p, 64, 0, o, 0, part) == -3);     // db needs ldo == N
+  CHECK(orion_gemm_colsum_scratch(65, 64) == (2 + 32) * 64);
   CHECK(orion_wgrad(p, 64, p, 64, 33, 64, 64, 1, nullptr, o, nullptr, 0, 0, 0) == -1);                 // M % BK
   CHECK(orion_wgrad(mis, 64, p, 64, 64, 64, 64, 1, nullptr, o, nullptr, 0, 0, 0) == -2);               // alignment
   CHECK(orion_wgrad(p, 64, p, 64, 4096, 64, 64, 2, nullptr, o, nullptr, 0, 0, 0) == -4);               // slabs missing

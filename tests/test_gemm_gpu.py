@@ -68,6 +68,55 @@ def test_gemm_gelu_backward_epilogue(M, N, K):
     assert rel_err(out, want) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 768), (4096, 3072, 768), (777, 264, 128)])
+@pytest.mark.parametrize("cfg", ["7", "8", "0"])
+@pytest.mark.parametrize("arena", [None, torch.float32, torch.bfloat16])
+def test_gemm_gelu_bwd_with_bias_grad(M, N, K, cfg, arena, monkeypatch):
+    """gemm_gelu_bwd: da = (dy w) * GELU'(pre + b) and db = colsum(da) (per-64-row partials
+    from the phased kernel's epilogue, cfg 7/8; a column-sum pass after csrc/gemm.hip's
+    kernel, cfg 0), db returned or written into a gradient-arena slice."""
+    monkeypatch.setenv("ORION_GEMM_CFG", cfg)
+    g = torch.Generator(device=DEV).manual_seed(M + N + 5 * K)
+    dy, w, pre, b = _rnd(g, M, K), _rnd(g, K, N), _rnd(g, M, N), _rnd(g, N)
+    want = (dy.float() @ w.float()) * _gelu_grad(pre.float() + b.float())
+    out = None if arena is None else torch.full((N,), 7.0, device=DEV, dtype=arena)
+    da, db = _C().gemm_gelu_bwd(dy, w, pre, b, out)
+    assert rel_err(da, want) < 1e-2
+    got = db if arena is None else out
+    assert (db is None or db.numel() == 0) if arena is not None else db.shape == (N,)
+    assert rel_err(got, want.sum(0)) < 1e-2
+
+
+def test_gemm_gelu_bwd_without_bias():
+    g = torch.Generator(device=DEV).manual_seed(21)
+    dy, w, pre = _rnd(g, 640, 256), _rnd(g, 256, 512), _rnd(g, 640, 512)
+    da, db = _C().gemm_gelu_bwd(dy, w, pre, None, None)
+    want = (dy.float() @ w.float()) * _gelu_grad(pre.float())
+    assert rel_err(da, want) < 1e-2
+    assert rel_err(db, want.sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("fuse_out_bias", [False, True])
+def test_fused_mlp_tail_matches_two_node_path(fuse_out_bias, monkeypatch):
+    """ops.gelu_linear (one autograd node, backward = one GEMM with GELU' and the fc-bias
+    gradient in its epilogue) against bias_gelu -> linear: output and every gradient."""
+    from orion_amd import ops
+    from orion_amd.ops import activations
+    g = torch.Generator(device=DEV).manual_seed(4)
+    a = _rnd(g, 2, 384, 3072)
+    bfc, w, b = _rnd(g, 3072), _rnd(g, 768, 3072) * 0.05, _rnd(g, 768)
+    dy = _rnd(g, 2, 384, 768)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(activations, "_FUSED_MLP", fused)
+        ts = [t.clone().requires_grad_() for t in (a, bfc, w, b)]
+        y = ops.gelu_linear(ts[0], ts[1], ts[2], None if fuse_out_bias else ts[3])
+        y.backward(dy)
+        res.append([y] + [t.grad for t in ts[:3]] + ([] if fuse_out_bias else [ts[3].grad]))
+    for name, x, y in zip(("y", "da", "dbfc", "dw", "db"), *res):
+        assert rel_err(x, y) < 1e-2, (name, rel_err(x, y))
+
+
 def test_gemm_batched_input_shape_and_strided_rows():
     g = torch.Generator(device=DEV).manual_seed(3)
     x = _rnd(g, 4, 96, 256)
