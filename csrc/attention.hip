@@ -867,7 +867,23 @@ static bool bwd_v2() {
   return v == 1;
 }
 
+int orion_attn_fwd3(const AttnParams& p, int D, bool causal, hipStream_t st);  // attn_fwd.hip
+
+// ORION_ATTN_FWD=v2 selects the kernel below (A/B measurement); default: attn_fwd.hip
+static bool fwd_v2() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORION_ATTN_FWD");
+    v = (e && e[0] == 'v' && e[1] == '2') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 int orion_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {
+  if (!fwd_v2()) {
+    const int r = orion_attn_fwd3(p, D, causal, st);
+    if (r != -2) return r;  // -2: offsets beyond 2 GB, the kernel below addresses 64-bit
+  }
   const int BM = 128;
   const int grid = ((p.T + BM - 1) / BM) * p.B * p.Hq;
 #define FWD(DD, CC)                                                                 \

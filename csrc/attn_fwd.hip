@@ -1,0 +1,296 @@
+// Flash-attention forward, round-3 form (gfx950): the algorithm of attention.hip's
+// attn_fwd_kernel (swapped S^T = K Q^T with the query on the lane, P straight from the
+// accumulator into O^T += V^T P^T, online softmax in base 2 with a deferred rescale) with
+// the per-tile instruction overhead taken out.  PMC of the older kernel at the GPT-2 shape
+// (profiles/pmc_attn_r02m.txt): 16 vector instructions per MFMA and 25 % MFMA busy -- the
+// kernel is bound by vector-instruction ISSUE, and half of those instructions were not
+// softmax but bookkeeping:
+//
+//   * K / V staging by buffer loads: one per-thread 32-bit offset computed once, the tile
+//     advance in the scalar soffset -- no 64-bit address multiply per load and tile (the
+//     clamped path runs only for a last partial tile);
+//   * the tile loop unrolled by the two LDS buffers, so every LDS read and write address is
+//     a loop-invariant per-lane register plus an immediate;
+//   * causal / length mask as one compare + select per score against a per-lane bound
+//     (the per-element key arithmetic and exec-mask branches are gone), on diagonal tiles
+//     only;
+//   * row max and row sum as four independent chains (no 32-deep dependent chain);
+//   * all K fragments of a tile read before its S MFMAs (ordered by sched_group_barrier),
+//     so the MFMAs no longer wait on one LDS round trip each.
+//
+// One workgroup = 4 waves = 128 query rows (32 per wave), key tiles of 64 double-buffered
+// in LDS, two workgroups per CU.  bf16 in / out, fp32 accumulation, O written as (B, T, H,
+// D), lse in base 2.  ORION_ATTN_FWD=v2 selects the older kernel (A/B measurement).
+#include <type_traits>
+
+#include "common.h"
+#include "attn_params.h"
+#include "mfma_lds.h"
+
+namespace orion {
+
+// Plain fmaxf / + here: this file is built with -fno-honor-nans (no canonicalising
+// v_max x, x per MFMA result, so max chains become v_max3) and -fno-slp-vectorize (adjacent
+// f32 adds are not packed into v_pk_add_f32, which costs more than two plain adds beside
+// MFMAs: MI355X_MICROARCH.md).  The same ops as inline asm miscomputed the diagonal tiles
+// (the asm hides the VALU result hazards from the compiler's wait-state insertion).
+ORION_DEVICE float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+ORION_DEVICE float addf(float a, float b) { return a + b; }
+
+// the two 32-lane halves of a wave exchanged by one v_permlane32_swap: {x of lanes 0-31,
+// x of lanes 32-63} in every lane (instead of __shfl_xor(x, 32)'s ds_bpermute round trip)
+ORION_DEVICE float half_max(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+ORION_DEVICE float half_sum(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+ORION_DEVICE bf16x8 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
+  constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int BH = p.B * p.Hq;
+  const int nqt = (p.T + BM - 1) / BM;
+  const int bh = blockIdx.x % BH;
+  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) tiles launch first
+  const int b = bh / p.Hq, hq = bh % p.Hq, hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qt * BM, qw0 = q0 + wv * 32;
+  const int off = p.Tk - p.T;  // causal: key <= query + off
+  const float c = p.scale_log2;
+  const int myq = qw0 + l32;
+
+  const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
+
+  bf16x8 qf[D / 16];
+  {
+    const int qr = min(myq, p.T - 1);
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks)
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * p.q_st + ks * 16 + 8 * h32);
+  }
+  const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
+  const int ntiles = (kend + BN - 1) / BN;
+
+  // staging: thread chunk i covers (row, ch) = ((tid + 256 i) / NCH, (tid + 256 i) % NCH)
+  const unsigned kst_b = (unsigned)p.k_st * 2, vst_b = (unsigned)p.v_st * 2;  // bytes per key row
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc(Kb, (unsigned)((long)(p.Tk - 1) * p.k_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(Vb, (unsigned)((long)(p.Tk - 1) * p.v_st + D) * 2);
+  unsigned vk[NST], vv[NST];
+  int lo[NST];
+#pragma unroll
+  for (int i = 0; i < NST; ++i) {
+    const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+    vk[i] = row * kst_b + ch * 16;
+    vv[i] = row * vst_b + ch * 16;
+    lo[i] = loff<D>(row, ch * 8);
+  }
+  bf16x8 kst[NST], vst[NST];
+  auto gload = [&](int t) {
+    if (t * BN + BN <= p.Tk) {
+      const unsigned sk = (unsigned)(t * BN) * kst_b, sv = (unsigned)(t * BN) * vst_b;
+#pragma unroll
+      for (int i = 0; i < NST; ++i) {
+        kst[i] = buf_load16(rk, vk[i], sk);
+        vst[i] = buf_load16(rv, vv[i], sv);
+      }
+    } else {  // last partial tile: rows past Tk re-read the last key (masked below)
+#pragma unroll
+      for (int i = 0; i < NST; ++i) {
+        const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+        const unsigned key = (unsigned)min(t * BN + row, p.Tk - 1);
+        kst[i] = buf_load16(rk, key * kst_b + ch * 16, 0);
+        vst[i] = buf_load16(rv, key * vst_b + ch * 16, 0);
+      }
+    }
+  };
+  auto swrite = [&](auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    bf16_t* Ks = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      *reinterpret_cast<bf16x8*>(Ks + lo[i]) = kst[i];
+      *reinterpret_cast<bf16x8*>(Ks + TILE + lo[i]) = vst[i];
+    }
+  };
+
+  // per-lane LDS fragment offsets (the same in both buffers)
+  int ko[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) ko[ks] = loff<D>(l32, ks * 16 + 8 * h32);
+
+  f32x16 oacc[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) oacc[db] = zero16();
+  float m = -1e30f, lsum = 0.f;
+
+  auto tile = [&](auto bufc, int t) {
+    constexpr int buf = decltype(bufc)::value;
+    if (t + 1 < ntiles) swrite(std::integral_constant<int, buf ^ 1>{});
+    if (t + 2 < ntiles) gload(t + 2);
+    const int k0 = t * BN;
+    const bf16_t* Ks = smem + buf * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+    const bool active = !CAUSAL || (k0 <= qw0 + 31 + off);
+    if (active) {
+      // K fragment reads issue before the S MFMAs that use them: all 8 at D = 64; one key
+      // block (8 of 16) at a time at D = 128, where 64 fragment registers would spill
+      constexpr int KBR = D == 64 ? 2 : 1;  // key blocks per read group
+      f32x16 s[2];
+#pragma unroll
+      for (int kg = 0; kg < 2; kg += KBR) {
+        bf16x8 kfr[KBR][D / 16];
+#pragma unroll
+        for (int kb = 0; kb < KBR; ++kb)
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) kfr[kb][ks] = lds_b128(Ks + (kg + kb) * 32 * D, ko[ks]);
+#pragma unroll
+        for (int kb = 0; kb < KBR; ++kb) {
+          s[kg + kb] = zero16();
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) s[kg + kb] = mfma32(kfr[kb][ks], qf[ks], s[kg + kb]);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, KBR * (D / 16), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KBR * (D / 16), 0);
+      }
+      const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw0 + off)) || (k0 + BN > p.Tk);
+      if (need_mask) {
+        // key k0 + kb*32 + rowoff(r) + 4*h32 is visible iff rowoff(r) <= lim
+        const int vis = CAUSAL ? min(myq + off, p.Tk - 1) : p.Tk - 1;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int lim = vis - (k0 + kb * 32 + 4 * h32);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            s[kb][r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[kb][r];
+        }
+      }
+      // row max: four independent 8-value chains of v_max3, then one combine
+      float mx4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x16& a = s[j >> 1];
+        const int r0 = (j & 1) * 8;
+        float x = max3f(a[r0], a[r0 + 1], a[r0 + 2]);
+        x = max3f(x, a[r0 + 3], a[r0 + 4]);
+        x = max3f(x, a[r0 + 5], a[r0 + 6]);
+        mx4[j] = max3f(x, a[r0 + 7], m);
+      }
+      float mx = max3f(mx4[0], mx4[1], max3f(mx4[2], mx4[3], m));
+      mx = half_max(mx);
+      // deferred rescale (see attn_fwd_kernel): the running max moves only when some row of
+      // the wave grew by more than 2^8
+      float alpha = 1.f;
+      if (__any((mx - m) * c > 8.f)) {
+        alpha = __builtin_amdgcn_exp2f((m - mx) * c);
+        m = mx;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+      }
+      const float mc = m * c;
+      float ps4[4] = {0.f, 0.f, 0.f, 0.f};
+      bf16x8 pf[4];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * s2 + j], c, -mc));
+            ps4[j & 3] = addf(ps4[j & 3], e);
+            pf[kb * 2 + s2][j] = f2bf(e);
+          }
+      lsum = fmaf(lsum, alpha, addf(addf(ps4[0], ps4[1]), addf(ps4[2], ps4[3])));
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        bf16x8 vfr[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) vfr[kk] = tr_frag<D>(Vs, kk * 16 + 4 * h32, db * 32, lane, 8);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) oacc[db] = mfma32(vfr[kk], pf[kk], oacc[db]);
+      }
+    }
+    __syncthreads();
+  };
+
+  gload(0);
+  swrite(std::integral_constant<int, 0>{});
+  // retire every prologue load (Q fragments included) with a wait the compiler's wait-count
+  // pass can see (see attn_fwd_kernel)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  if (ntiles > 1) gload(1);
+  __syncthreads();
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
+  }
+
+  const float lt = half_sum(lsum);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (myq < p.T) {
+    bf16_t* Ob = p.o + b * p.o_sb + hq * p.o_sh + (long)myq * p.o_st;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(oacc[db][4 * g4 + j] * inv);
+        *reinterpret_cast<bf16x4*>(Ob + db * 32 + 8 * g4 + 4 * h32) = v4;
+      }
+    if (h32 == 0) p.lse[((long)b * p.Hq + hq) * p.T + myq] = m * c + __log2f(lt);
+  }
+}
+
+}  // namespace orion
+
+using namespace orion;
+
+extern "C++" {
+
+template <int D, bool CAUSAL>
+static void fwd3_attr() {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd3_kernel<D, CAUSAL>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 64 * D * 2);
+    done = true;
+  }
+}
+
+// returns -1 for an unsupported head dim, -2 when the buffer-offset range is exceeded
+// (the caller falls back to the older kernel)
+int orion_attn_fwd3(const AttnParams& p, int D, bool causal, hipStream_t st) {
+  const long kbytes = ((long)(p.Tk - 1) * p.k_st + D) * 2, vbytes = ((long)(p.Tk - 1) * p.v_st + D) * 2;
+  if (kbytes >= (1L << 31) || vbytes >= (1L << 31)) return -2;
+  const int grid = ((p.T + 127) / 128) * p.B * p.Hq;
+  const size_t lds = (size_t)2 * 2 * 64 * D * 2;
+#define FWD3(DD, CC)                                                                \
+  fwd3_attr<DD, CC>();                                                              \
+  attn_fwd3_kernel<DD, CC><<<grid, 256, lds, st>>>(p);
+  if (D == 64) {
+    if (causal) { FWD3(64, true) } else { FWD3(64, false) }
+  } else if (D == 128) {
+    if (causal) { FWD3(128, true) } else { FWD3(128, false) }
+  } else {
+    return -1;
+  }
+#undef FWD3
+  return (int)hipGetLastError();
+}
+
+}  // extern "C++"

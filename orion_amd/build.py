@@ -41,6 +41,10 @@ def _torch_paths():
     return ce.include_paths(), ce.library_paths(), abi
 
 
+# per-source extra flags (see the comment at the top of each file)
+FILE_FLAGS = {"attn_fwd.hip": ["-fno-honor-nans", "-fno-slp-vectorize"]}
+
+
 def _newest_header():
     hs = glob.glob(os.path.join(CSRC, "*.h"))
     return max((os.path.getmtime(h) for h in hs), default=0.0)
@@ -76,7 +80,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
             os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_time)
         if stale:
             base = bind if src.endswith(".cpp") else kern
-            jobs_list.append(base + ["-c", src, "-o", obj])
+            jobs_list.append(base + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj])
     jobs = jobs or min(8, os.cpu_count() or 4)
     if jobs_list:
         with cf.ThreadPoolExecutor(jobs) as ex:

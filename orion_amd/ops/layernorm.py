@@ -78,6 +78,9 @@ class _AddLayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, r, w, b, rb, eps):
         s, y, mean, rstd = C().add_layernorm_fwd(x, r, _bf16(w), _bf16(b), float(eps), _bf16(rb))
+        # an unused output (the last block's residual sum) arrives as None, not as a
+        # materialised zero tensor (a 100 MB fill + read per step on GPT-2)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(s, w, mean, rstd)
         ctx.has_bias = b is not None
         ctx.b_dtype = None if b is None else b.dtype
@@ -176,6 +179,7 @@ class _AddRMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, r, w, eps):
         s, y, rstd = C().add_rmsnorm_fwd(x, r, _bf16(w), float(eps))
+        ctx.set_materialize_grads(False)  # see _AddLayerNorm
         ctx.save_for_backward(s, w, rstd)
         ctx.params = (w,)
         return s.view(x.shape), y.view(x.shape)

@@ -2,6 +2,12 @@
 """Condense a rocprofv3 kernel_stats.csv: per-step ms per kernel (short names) and per category.
 
 usage: python scripts/prof_summary.py gpurun_out/prof/run_kernel_stats.csv --steps 5
+       python scripts/prof_summary.py gpurun_out/prof/run_kernel_trace.csv --steady
+
+``--steady`` reads the kernel TRACE instead and counts only the kernels dispatched after the
+first optimizer step's AdamW kernel up to and including the last one: whole steady-state
+steps, without model construction, arena initialisation or first-step allocations (which a
+stats file averaged over all steps folds into the per-step numbers).
 """
 import argparse
 import csv
@@ -34,18 +40,30 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--steady", action="store_true", help="trace CSV: steady-state steps only")
     a = ap.parse_args()
     rows = []
-    with open(a.csv) as f:
-        for r in csv.DictReader(f):
-            rows.append((short(r["Name"]), int(r["Calls"]), float(r["TotalDurationNs"]) / 1e6))
+    if a.steady:
+        with open(a.csv) as f:
+            tr = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
+        ends = [i for i, r in enumerate(tr) if "adamw_flat" in r["Kernel_Name"]]
+        if len(ends) < 2:
+            raise SystemExit("--steady needs a trace with at least two optimizer steps")
+        a.steps = len(ends) - 1
+        for r in tr[ends[0] + 1: ends[-1] + 1]:
+            rows.append((short(r["Kernel_Name"]), 1,
+                         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    else:
+        with open(a.csv) as f:
+            for r in csv.DictReader(f):
+                rows.append((short(r["Name"]), int(r["Calls"]), float(r["TotalDurationNs"]) / 1e6))
     agg = {}
     for n, c, t in rows:
         k = agg.setdefault(n, [0, 0.0])
         k[0] += c
         k[1] += t
     tot = sum(v[1] for v in agg.values())
-    print(f"total {tot / a.steps:.2f} ms/step over {a.steps} steps")
+    print(f"total {tot / a.steps:.2f} ms/step over {a.steps} {'steady-state ' if a.steady else ''}steps")
     print(f"{'kernel':72s} {'calls/st':>8s} {'ms/step':>8s} {'%':>6s}")
     for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"{n:72s} {c / a.steps:8.1f} {t / a.steps:8.3f} {100 * t / tot:6.2f}")
