@@ -22,6 +22,8 @@
 //                  bf16 dQ written once -- no fp32 accumulator, no conversion pass.
 //
 // MFMA v_mfma_f32_32x32x16_bf16 throughout; LDS images and fragment helpers: mfma_lds.h.
+#include <type_traits>
+
 #include "common.h"
 #include "attn_params.h"
 #include "mfma_lds.h"
@@ -46,6 +48,11 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* __
 #pragma unroll
   for (int o2 = TPR / 2; o2 > 0; o2 >>= 1) s += __shfl_xor(s, o2, 64);
   if (row < nrows && sub == 0) delta[row] = s;
+}
+
+// 16 bytes per lane by a raw buffer load (scalar soffset carries the tile position)
+ORION_DEVICE bf16x8 bwd_buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
 // ============================================================================ dK / dV
@@ -117,25 +124,56 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 
   bf16x8 qdst[NSTQ];
   float lse_r = 0.f, del_r = 0.f;
-  // (head, query tile) of a loop step, walked incrementally (no integer division per tile)
+  // Q / dO tiles by buffer loads over this batch's rows of all query heads: one per-thread
+  // 32-bit offset (its row / chunk in the tile), the (head, tile) position in the scalar
+  // offset; the clamped path runs only for a last partial query tile
+  const bf16_t* Qbb = p.q + b * p.q_sb;
+  const bf16_t* Dbb = p.dout + b * p.do_sb;
+  const __amdgpu_buffer_rsrc_t rq =
+      make_rsrc(Qbb, (unsigned)(((long)(p.T - 1) * p.q_st + (long)(p.Hq - 1) * p.q_sh + D) * 2));
+  const __amdgpu_buffer_rsrc_t rd =
+      make_rsrc(Dbb, (unsigned)(((long)(p.T - 1) * p.do_st + (long)(p.Hq - 1) * p.do_sh + D) * 2));
+  constexpr int NQ = NSTQ >= 2 ? NSTQ / 2 : 1;  // chunks per thread per tensor
+  unsigned vq[NQ];
+  // this thread's tile row / 16-byte chunk for chunk i (recomputed where needed: registers
+  // are short at D = 128)
+  auto qrow = [&](int i) { return NSTQ >= 2 ? (tid + i * NT) / NCH : (tid - (tid >= NQC) * NQC) / NCH; };
+  auto qch = [&](int i) { return NSTQ >= 2 ? (tid + i * NT) % NCH : (tid - (tid >= NQC) * NQC) % NCH; };
+  const bool isd = NSTQ < 2 && tid >= NQC;
+  const unsigned qst_b = (unsigned)(isd ? p.do_st : p.q_st) * 2, dst_b = (unsigned)p.do_st * 2;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) vq[i] = qrow(i) * (NSTQ >= 2 ? (unsigned)p.q_st * 2 : qst_b) + qch(i) * 16;
+  unsigned vdo[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) vdo[i] = qrow(i) * dst_b + qch(i) * 16;
   auto gload = [&](int h, int qi) {
     const int hq = hk * rep + h;
     const int qbase = qi * BMQ;
-    const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
-    const bf16_t* Db = p.dout + b * p.do_sb + hq * p.do_sh;
-    if constexpr (NSTQ >= 2) {
+    const unsigned sq = (unsigned)((long)hq * p.q_sh + (long)qbase * p.q_st) * 2;
+    const unsigned sd = (unsigned)((long)hq * p.do_sh + (long)qbase * p.do_st) * 2;
+    if (qbase + BMQ <= p.T) {
+      if constexpr (NSTQ >= 2) {
 #pragma unroll
-      for (int i = 0; i < NSTQ / 2; ++i) {
-        const int cc = tid + i * NT, row = cc / NCH, ch = cc % NCH;
-        const long q = min(qbase + row, p.T - 1);
-        qdst[i] = *reinterpret_cast<const bf16x8*>(Qb + q * p.q_st + ch * 8);
-        qdst[NSTQ / 2 + i] = *reinterpret_cast<const bf16x8*>(Db + q * p.do_st + ch * 8);
+        for (int i = 0; i < NQ; ++i) {
+          qdst[i] = bwd_buf_load16(rq, vq[i], sq);
+          qdst[NQ + i] = bwd_buf_load16(rd, vdo[i], sd);
+        }
+      } else {
+        qdst[0] = isd ? bwd_buf_load16(rd, vq[0], sd) : bwd_buf_load16(rq, vq[0], sq);
       }
-    } else {  // one chunk per thread: the first NQC threads take Q, the rest dO
-      const int isd = tid >= NQC, w = tid - isd * NQC;
-      const long q = min(qbase + w / NCH, p.T - 1);
-      const bf16_t* src = isd ? Db + q * p.do_st : Qb + q * p.q_st;
-      qdst[0] = *reinterpret_cast<const bf16x8*>(src + (w % NCH) * 8);
+    } else {  // rows past T re-read the last query row (masked in the step)
+      const unsigned sq0 = (unsigned)((long)hq * p.q_sh) * 2, sd0 = (unsigned)((long)hq * p.do_sh) * 2;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const unsigned q = (unsigned)min(qbase + qrow(i), p.T - 1);
+        if constexpr (NSTQ >= 2) {
+          qdst[i] = bwd_buf_load16(rq, q * (unsigned)p.q_st * 2 + qch(i) * 16, sq0);
+          qdst[NQ + i] = bwd_buf_load16(rd, q * dst_b + qch(i) * 16, sd0);
+        } else {
+          qdst[0] = isd ? bwd_buf_load16(rd, q * dst_b + qch(0) * 16, sd0)
+                        : bwd_buf_load16(rq, q * (unsigned)p.q_st * 2 + qch(0) * 16, sq0);
+        }
+      }
     }
     if (tid < BMQ) {
       const long q = min(qbase + tid, p.T - 1);
@@ -144,17 +182,18 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
       del_r = p.delta[r];
     }
   };
+  int qlo_[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) qlo_[i] = loff<D>(qrow(i), qch(i) * 8);
   auto swrite = [&](int buf) {
     if constexpr (NSTQ >= 2) {
 #pragma unroll
-      for (int i = 0; i < NSTQ / 2; ++i) {
-        const int cc = tid + i * NT, o = loff<D>(cc / NCH, (cc % NCH) * 8);
-        *reinterpret_cast<bf16x8*>(Qs + buf * QT + o) = qdst[i];
-        *reinterpret_cast<bf16x8*>(Ds + buf * QT + o) = qdst[NSTQ / 2 + i];
+      for (int i = 0; i < NQ; ++i) {
+        *reinterpret_cast<bf16x8*>(Qs + buf * QT + qlo_[i]) = qdst[i];
+        *reinterpret_cast<bf16x8*>(Ds + buf * QT + qlo_[i]) = qdst[NQ + i];
       }
     } else {
-      const int isd = tid >= NQC, w = tid - isd * NQC;
-      *reinterpret_cast<bf16x8*>((isd ? Ds : Qs) + buf * QT + loff<D>(w / NCH, (w % NCH) * 8)) = qdst[0];
+      *reinterpret_cast<bf16x8*>((isd ? Ds : Qs) + buf * QT + qlo_[0]) = qdst[0];
     }
     if (tid < BMQ) {  // row constants as the initial S / dP accumulators
       lse_s[buf * BMQ + tid] = -lse_r * inv_c;
@@ -208,13 +247,20 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
       // P and dS in place: row q = qbase + (r&3)+8(r>>2)+4*h32, column = mykey
       const bool need_mask = (CAUSAL && (qbase + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
                              (qbase + BMQ > p.T);
+      if (need_mask) {
+        // row q = qbase + rowoff(r) + 4*h32 contributes iff lo <= rowoff(r) < hi
+        const int q4 = qbase + 4 * h32;
+        const int lo = CAUSAL ? mykey - off - q4 : 0;
+        const int hi = mykey < p.Tk ? p.T - q4 : 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          s[r] = (ro < lo || ro >= hi) ? -INFINITY : s[r];
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float pv = __builtin_amdgcn_exp2f(s[r] * c);
-        if (need_mask) {
-          const int q = qbase + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          if (mykey >= p.Tk || q >= p.T || (CAUSAL && mykey > q + off)) pv = 0.f;
-        }
+        const float pv = __builtin_amdgcn_exp2f(s[r] * c);
         s[r] = pv;
         dp[r] = pv * dp[r];  // dS / scale: the scale is applied to dK once at the end
       }
@@ -258,6 +304,10 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 
 // ============================================================================ dQ
 // One 256-thread workgroup = 4 waves x 32 queries; key tiles of 64 double-buffered in LDS.
+// Per-tile bookkeeping as in attn_fwd.hip's forward: K / V staged by buffer loads with the
+// tile advance in the scalar offset, the tile loop unrolled over the two LDS buffers (every
+// LDS address a per-lane register plus an immediate), the causal / length mask one
+// compare + select per score against a per-lane bound.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
@@ -295,43 +345,61 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
   const int ntiles = (kend + BN - 1) / BN;
 
+  const unsigned kst_b = (unsigned)p.k_st * 2, vst_b = (unsigned)p.v_st * 2;
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc(Kb, (unsigned)((long)(p.Tk - 1) * p.k_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(Vb, (unsigned)((long)(p.Tk - 1) * p.v_st + D) * 2);
+  unsigned vk[NST], vv[NST];
+  int lo[NST];
+#pragma unroll
+  for (int i = 0; i < NST; ++i) {
+    const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+    vk[i] = row * kst_b + ch * 16;
+    vv[i] = row * vst_b + ch * 16;
+    lo[i] = loff<D>(row, ch * 8);
+  }
   bf16x8 kst[NST], vst[NST];
   auto gload = [&](int t) {
+    if (t * BN + BN <= p.Tk) {
+      const unsigned sk = (unsigned)(t * BN) * kst_b, sv = (unsigned)(t * BN) * vst_b;
 #pragma unroll
-    for (int i = 0; i < NST; ++i) {
-      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
-      const long key = min(t * BN + row, p.Tk - 1);
-      ORION_DASSERT(key >= 0 && ch * 8 + 8 <= D);
-      kst[i] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ch * 8);
-      vst[i] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ch * 8);
+      for (int i = 0; i < NST; ++i) {
+        kst[i] = bwd_buf_load16(rk, vk[i], sk);
+        vst[i] = bwd_buf_load16(rv, vv[i], sv);
+      }
+    } else {  // last partial tile: rows past Tk re-read the last key (masked below)
+#pragma unroll
+      for (int i = 0; i < NST; ++i) {
+        const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
+        const unsigned key = (unsigned)min(t * BN + row, p.Tk - 1);
+        kst[i] = bwd_buf_load16(rk, key * kst_b + ch * 16, 0);
+        vst[i] = bwd_buf_load16(rv, key * vst_b + ch * 16, 0);
+      }
     }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
     bf16_t* Ks = smem + buf * 2 * TILE;
-    bf16_t* Vs = Ks + TILE;
 #pragma unroll
     for (int i = 0; i < NST; ++i) {
-      const int cidx = tid + i * 256, row = cidx / NCH, ch = cidx % NCH;
-      const int o = loff<D>(row, ch * 8);
-      *reinterpret_cast<bf16x8*>(Ks + o) = kst[i];
-      *reinterpret_cast<bf16x8*>(Vs + o) = vst[i];
+      *reinterpret_cast<bf16x8*>(Ks + lo[i]) = kst[i];
+      *reinterpret_cast<bf16x8*>(Ks + TILE + lo[i]) = vst[i];
     }
   };
+  int ko[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) ko[ks] = loff<D>(l32, ks * 16 + 8 * h32);
+  // key k0 + rowoff(r) + 4*h32 of a 32-key block is visible to this lane's query iff
+  // rowoff(r) <= vis - k0 - 4*h32
+  const int vis = (CAUSAL ? min(myq + off, p.Tk - 1) : p.Tk - 1) - 4 * h32;
 
   f32x16 dq[NDB];
 #pragma unroll
   for (int db = 0; db < NDB; ++db) dq[db] = zero16();
 
-  if (ntiles > 0) {
-    gload(0);
-    swrite(0);
-  }
-  // retire the prologue loads with a wait the compiler can see (see attn_fwd_kernel)
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  auto tile = [&](auto bufc, int t) {
+    constexpr int buf = decltype(bufc)::value;
     if (t + 1 < ntiles) gload(t + 1);
-    const bf16_t* Ks = smem + (t & 1) * 2 * TILE;
+    const bf16_t* Ks = smem + buf * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -340,20 +408,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        const int o = loff<D>(kb * 32 + l32, ks * 16 + 8 * h32);
-        s = mfma32(lds_b128(Ks, o), qf[ks], s);
-        dp = mfma32(lds_b128(Vs, o), df[ks], dp);
+        s = mfma32(lds_b128(Ks + kb * 32 * D, ko[ks]), qf[ks], s);
+        dp = mfma32(lds_b128(Vs + kb * 32 * D, ko[ks]), df[ks], dp);
         if constexpr (D == 128) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
       }
       // S^T / dP^T: row = key k0 + (r&3)+8(r>>2)+4*h32, column = this lane's query
       const bool need_mask = (CAUSAL && (k0 + 31 > qw0 + off)) || (k0 + 32 > p.Tk);
+      if (need_mask) {
+        const int lim = vis - k0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          s[r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[r];
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c, -L));
-        if (need_mask) {
-          const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          if (key >= p.Tk || (CAUSAL && key > myq + off)) pv = 0.f;
-        }
+        const float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c, -L));
         dp[r] = pv * (dp[r] - dl);  // dS^T / scale
       }
       const bf16x8 ds0 = acc_to_frag(dp, 0), ds1 = acc_to_frag(dp, 1);
@@ -365,8 +434,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
         dq[db] = mfma32(tr_frag<D>(Ks, kb * 32 + 16 + 4 * h32, db * 32, lane, 8), ds1, dq[db]);
       }
     }
-    if (t + 1 < ntiles) swrite((t + 1) & 1);
+    if (t + 1 < ntiles) swrite(std::integral_constant<int, buf ^ 1>{});
     __syncthreads();
+  };
+
+  if (ntiles > 0) {
+    gload(0);
+    swrite(std::integral_constant<int, 0>{});
+  }
+  // retire the prologue loads with a wait the compiler can see (see attn_fwd_kernel)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
   }
 
   if (myq < p.T) {
@@ -410,6 +491,9 @@ static void split_attrs() {
 // delta (caller-allocated [B][Hq][T] fp32) then dK/dV and dQ; p.dq / dk / dv are bf16
 // outputs (strided views allowed).  kv and dq launches are independent after delta.
 int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
+  // the dQ kernel addresses one (batch, KV head)'s K / V with 32-bit buffer offsets
+  if (((long)(p.Tk - 1) * p.k_st + D) * 2 >= (1L << 31) || ((long)(p.Tk - 1) * p.v_st + D) * 2 >= (1L << 31))
+    return -2;
   const long rows = (long)p.B * p.Hq * p.T;
   const int pre_grid = (int)((rows * (D / 8) + 255) / 256);
   AttnParams q = p;
