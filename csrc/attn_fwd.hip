@@ -21,6 +21,7 @@
 // One workgroup = 4 waves = 128 query rows (32 per wave), key tiles of 64 double-buffered
 // in LDS, two workgroups per CU.  bf16 in / out, fp32 accumulation, O written as (B, T, H,
 // D), lse in base 2.  ORION_ATTN_FWD=v2 selects the older kernel (A/B measurement).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -54,9 +55,11 @@ ORION_DEVICE bf16x8 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int QB>
 __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
-  constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
+  // QB query blocks of 32 rows per wave (D = 64: 2, one 64-key tile's K / V fragments feed
+  // both blocks' MFMAs and the two softmax chains interleave with each other's MFMAs)
+  constexpr int BM = 128 * QB, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h32 = lane >> 5, l32 = lane & 31;
@@ -65,21 +68,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
   const int bh = blockIdx.x % BH;
   const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) tiles launch first
   const int b = bh / p.Hq, hq = bh % p.Hq, hk = hq / (p.Hq / p.Hkv);
-  const int q0 = qt * BM, qw0 = q0 + wv * 32;
+  const int q0 = qt * BM, qw0 = q0 + wv * 32 * QB;
   const int off = p.Tk - p.T;  // causal: key <= query + off
   const float c = p.scale_log2;
-  const int myq = qw0 + l32;
 
   const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
   const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
 
-  bf16x8 qf[D / 16];
-  {
-    const int qr = min(myq, p.T - 1);
+  bf16x8 qf[QB][D / 16];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const int qr = min(qw0 + qb * 32 + l32, p.T - 1);
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks)
-      qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * p.q_st + ks * 16 + 8 * h32);
+      qf[qb][ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * p.q_st + ks * 16 + 8 * h32);
   }
   const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
   const int ntiles = (kend + BN - 1) / BN;
@@ -131,10 +134,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) ko[ks] = loff<D>(l32, ks * 16 + 8 * h32);
 
-  f32x16 oacc[NDB];
+  f32x16 oacc[QB][NDB];
+  float m[QB], lsum[QB];
 #pragma unroll
-  for (int db = 0; db < NDB; ++db) oacc[db] = zero16();
-  float m = -1e30f, lsum = 0.f;
+  for (int qb = 0; qb < QB; ++qb) {
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) oacc[qb][db] = zero16();
+    m[qb] = -1e30f;
+    lsum[qb] = 0.f;
+  }
 
   auto tile = [&](auto bufc, int t) {
     constexpr int buf = decltype(bufc)::value;
@@ -143,12 +151,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
     const int k0 = t * BN;
     const bf16_t* Ks = smem + buf * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
-    const bool active = !CAUSAL || (k0 <= qw0 + 31 + off);
+    const bool active = !CAUSAL || (k0 <= qw0 + 32 * QB - 1 + off);
     if (active) {
       // K fragment reads issue before the S MFMAs that use them: all 8 at D = 64; one key
       // block (8 of 16) at a time at D = 128, where 64 fragment registers would spill
       constexpr int KBR = D == 64 ? 2 : 1;  // key blocks per read group
-      f32x16 s[2];
+      f32x16 s[QB][2];
 #pragma unroll
       for (int kg = 0; kg < 2; kg += KBR) {
         bf16x8 kfr[KBR][D / 16];
@@ -157,71 +165,80 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
 #pragma unroll
           for (int ks = 0; ks < D / 16; ++ks) kfr[kb][ks] = lds_b128(Ks + (kg + kb) * 32 * D, ko[ks]);
 #pragma unroll
-        for (int kb = 0; kb < KBR; ++kb) {
-          s[kg + kb] = zero16();
+        for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) s[kg + kb] = mfma32(kfr[kb][ks], qf[ks], s[kg + kb]);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, KBR * (D / 16), 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, KBR * (D / 16), 0);
-      }
-      const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw0 + off)) || (k0 + BN > p.Tk);
-      if (need_mask) {
-        // key k0 + kb*32 + rowoff(r) + 4*h32 is visible iff rowoff(r) <= lim
-        const int vis = CAUSAL ? min(myq + off, p.Tk - 1) : p.Tk - 1;
+          for (int kb = 0; kb < KBR; ++kb) {
+            s[qb][kg + kb] = zero16();
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          const int lim = vis - (k0 + kb * 32 + 4 * h32);
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            s[kb][r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[kb][r];
-        }
-      }
-      // row max: four independent 8-value chains of v_max3, then one combine
-      float mx4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x16& a = s[j >> 1];
-        const int r0 = (j & 1) * 8;
-        float x = max3f(a[r0], a[r0 + 1], a[r0 + 2]);
-        x = max3f(x, a[r0 + 3], a[r0 + 4]);
-        x = max3f(x, a[r0 + 5], a[r0 + 6]);
-        mx4[j] = max3f(x, a[r0 + 7], m);
-      }
-      float mx = max3f(mx4[0], mx4[1], max3f(mx4[2], mx4[3], m));
-      mx = half_max(mx);
-      // deferred rescale (see attn_fwd_kernel): the running max moves only when some row of
-      // the wave grew by more than 2^8
-      float alpha = 1.f;
-      if (__any((mx - m) * c > 8.f)) {
-        alpha = __builtin_amdgcn_exp2f((m - mx) * c);
-        m = mx;
-#pragma unroll
-        for (int db = 0; db < NDB; ++db)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-      }
-      const float mc = m * c;
-      float ps4[4] = {0.f, 0.f, 0.f, 0.f};
-      bf16x8 pf[4];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * s2 + j], c, -mc));
-            ps4[j & 3] = addf(ps4[j & 3], e);
-            pf[kb * 2 + s2][j] = f2bf(e);
+            for (int ks = 0; ks < D / 16; ++ks) s[qb][kg + kb] = mfma32(kfr[kb][ks], qf[qb][ks], s[qb][kg + kb]);
           }
-      lsum = fmaf(lsum, alpha, addf(addf(ps4[0], ps4[1]), addf(ps4[2], ps4[3])));
+        __builtin_amdgcn_sched_group_barrier(0x100, KBR * (D / 16), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, QB * KBR * (D / 16), 0);
+      }
+      bf16x8 pf[QB][4];
+      float alpha[QB];
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const int qwb = qw0 + qb * 32;
+        const bool need_mask = (CAUSAL && (k0 + BN - 1 > qwb + off)) || (k0 + BN > p.Tk);
+        if (need_mask) {
+          // key k0 + kb*32 + rowoff(r) + 4*h32 is visible iff rowoff(r) <= lim
+          const int vis = CAUSAL ? min(qwb + l32 + off, p.Tk - 1) : p.Tk - 1;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            const int lim = vis - (k0 + kb * 32 + 4 * h32);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              s[qb][kb][r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[qb][kb][r];
+          }
+        }
+        // row max: four independent 8-value chains of v_max3, then one combine
+        float mx4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x16& a = s[qb][j >> 1];
+          const int r0 = (j & 1) * 8;
+          float x = max3f(a[r0], a[r0 + 1], a[r0 + 2]);
+          x = max3f(x, a[r0 + 3], a[r0 + 4]);
+          x = max3f(x, a[r0 + 5], a[r0 + 6]);
+          mx4[j] = max3f(x, a[r0 + 7], m[qb]);
+        }
+        float mx = max3f(mx4[0], mx4[1], max3f(mx4[2], mx4[3], m[qb]));
+        mx = half_max(mx);
+        // deferred rescale (see attn_fwd_kernel): the running max moves only when some row
+        // of the block grew by more than 2^8
+        alpha[qb] = 1.f;
+        if (__any((mx - m[qb]) * c > 8.f)) {
+          alpha[qb] = __builtin_amdgcn_exp2f((m[qb] - mx) * c);
+          m[qb] = mx;
+#pragma unroll
+          for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[qb][db][r] *= alpha[qb];
+        }
+        const float mc = m[qb] * c;
+        float ps4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float e = __builtin_amdgcn_exp2f(fmaf(s[qb][kb][8 * s2 + j], c, -mc));
+              ps4[j & 3] = addf(ps4[j & 3], e);
+              pf[qb][kb * 2 + s2][j] = f2bf(e);
+            }
+        lsum[qb] = fmaf(lsum[qb], alpha[qb], addf(addf(ps4[0], ps4[1]), addf(ps4[2], ps4[3])));
+      }
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
         bf16x8 vfr[4];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) vfr[kk] = tr_frag<D>(Vs, kk * 16 + 4 * h32, db * 32, lane, 8);
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) oacc[db] = mfma32(vfr[kk], pf[kk], oacc[db]);
+        for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) oacc[qb][db] = mfma32(vfr[kk], pf[qb][kk], oacc[qb][db]);
       }
     }
     __syncthreads();
@@ -239,20 +256,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
     if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
   }
 
-  const float lt = half_sum(lsum);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (myq < p.T) {
-    bf16_t* Ob = p.o + b * p.o_sb + hq * p.o_sh + (long)myq * p.o_st;
 #pragma unroll
-    for (int db = 0; db < NDB; ++db)
+  for (int qb = 0; qb < QB; ++qb) {
+    const int myq = qw0 + qb * 32 + l32;
+    const float lt = half_sum(lsum[qb]);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    if (myq < p.T) {
+      bf16_t* Ob = p.o + b * p.o_sb + hq * p.o_sh + (long)myq * p.o_st;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        bf16x4 v4;
+      for (int db = 0; db < NDB; ++db)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = f2bf(oacc[db][4 * g4 + j] * inv);
-        *reinterpret_cast<bf16x4*>(Ob + db * 32 + 8 * g4 + 4 * h32) = v4;
-      }
-    if (h32 == 0) p.lse[((long)b * p.Hq + hq) * p.T + myq] = m * c + __log2f(lt);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          bf16x4 v4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v4[j] = f2bf(oacc[qb][db][4 * g4 + j] * inv);
+          *reinterpret_cast<bf16x4*>(Ob + db * 32 + 8 * g4 + 4 * h32) = v4;
+        }
+      if (h32 == 0) p.lse[((long)b * p.Hq + hq) * p.T + myq] = m[qb] * c + __log2f(lt);
+    }
   }
 }
 
@@ -262,14 +283,27 @@ using namespace orion;
 
 extern "C++" {
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int QB>
 static void fwd3_attr() {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd3_kernel<D, CAUSAL>,
+    (void)hipFuncSetAttribute((const void*)attn_fwd3_kernel<D, CAUSAL, QB>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 64 * D * 2);
     done = true;
   }
+}
+
+template <int D, bool CAUSAL>
+static void fwd3_launch(const AttnParams& p, int qb64, size_t lds, hipStream_t st) {
+  if constexpr (D == 64) {
+    if (qb64 == 2) {
+      fwd3_attr<D, CAUSAL, 2>();
+      attn_fwd3_kernel<D, CAUSAL, 2><<<((p.T + 255) / 256) * p.B * p.Hq, 256, lds, st>>>(p);
+      return;
+    }
+  }
+  fwd3_attr<D, CAUSAL, 1>();
+  attn_fwd3_kernel<D, CAUSAL, 1><<<((p.T + 127) / 128) * p.B * p.Hq, 256, lds, st>>>(p);
 }
 
 // returns -1 for an unsupported head dim, -2 when the buffer-offset range is exceeded
@@ -277,11 +311,13 @@ static void fwd3_attr() {
 int orion_attn_fwd3(const AttnParams& p, int D, bool causal, hipStream_t st) {
   const long kbytes = ((long)(p.Tk - 1) * p.k_st + D) * 2, vbytes = ((long)(p.Tk - 1) * p.v_st + D) * 2;
   if (kbytes >= (1L << 31) || vbytes >= (1L << 31)) return -2;
-  const int grid = ((p.T + 127) / 128) * p.B * p.Hq;
   const size_t lds = (size_t)2 * 2 * 64 * D * 2;
-#define FWD3(DD, CC)                                                                \
-  fwd3_attr<DD, CC>();                                                              \
-  attn_fwd3_kernel<DD, CC><<<grid, 256, lds, st>>>(p);
+  // ORION_FWD_QB=2: two 32-row query blocks per wave at D = 64 (one K / V fragment read for
+  // both, the two softmax chains interleaved with each other's MFMAs; 255 VGPRs).  Measured
+  // equal to one block per wave at the GPT-2 shape (0.208-0.211 vs 0.209-0.217 ms, three
+  // alternating runs), so one block (BM = 128: finer causal balance) stays the default.
+  static const int qb64 = getenv("ORION_FWD_QB") && getenv("ORION_FWD_QB")[0] == '2' ? 2 : 1;
+#define FWD3(DD, CC) fwd3_launch<DD, CC>(p, qb64, lds, st);
   if (D == 64) {
     if (causal) { FWD3(64, true) } else { FWD3(64, false) }
   } else if (D == 128) {

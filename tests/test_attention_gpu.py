@@ -145,3 +145,20 @@ def test_forward_deferred_rescale_growing_scores(D, causal):
     o, _ = _C().attn_fwd(q, k, v, causal, 1.0 / math.sqrt(D))
     want = ref.attention(q.float(), k.float(), v.float(), causal)
     assert rel_err(o, want) < 3e-2
+
+
+@pytest.mark.parametrize("env", [{"ORION_FWD_QB": "2"}, {"ORION_ATTN_FWD": "v2"}])
+def test_forward_kernel_variants_match_reference(env):
+    """The non-default forward kernels (two query blocks per wave; the older attention.hip
+    kernel) on causal / full, D 64 / 128, GQA and ragged T.  The selection is read once per
+    process, so each variant runs in a child process (scripts/attn_fwd_diff.py)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "attn_fwd_diff.py")],
+                       env={**os.environ, **env}, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if "max err" in ln]
+    assert len(lines) == 7, r.stdout
+    assert all("bad rows 0 /" in ln for ln in lines), r.stdout
