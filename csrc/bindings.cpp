@@ -18,7 +18,10 @@
 
 // launchers (csrc/*.hip)
 int orion_layernorm_fwd(const void*, const void*, const void*, void*, float*, float*, int, int,
-                        float, const void*, void*, const void*, hipStream_t);
+                        float, const void*, void*, const void*, hipStream_t,
+                        const int64_t* idx = nullptr, int T = 0);
+int orion_embed_scatter_add(const void*, const int64_t*, float*, long, int, hipStream_t);
+int orion_batch_sum(const void*, void*, int, long, int, hipStream_t);
 int orion_layernorm_bwd_blocks(int rows);
 int orion_layernorm_bwd(const void*, const void*, const void*, const float*, const float*, void*,
                         void*, void*, float*, int, int, const void*, void*, int, hipStream_t);
@@ -152,6 +155,70 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_layernorm_fwd(const Tensor& x, co
                                    rbc.defined() ? rbc.data_ptr() : nullptr, cur_stream()),
                "add_layernorm_fwd");
   return {sum, y, mean, rstd};
+}
+
+// s = wte[idx] + wpe[t] ; y = LayerNorm(s)  -> (s, y, mean, rstd); idx (B, T) int64
+std::tuple<Tensor, Tensor, Tensor, Tensor> embed_layernorm_fwd(const Tensor& idx, const Tensor& wte,
+                                                               const Tensor& wpe, const Tensor& w,
+                                                               const c10::optional<Tensor>& b,
+                                                               double eps) {
+  check_bf16(wte, "wte");
+  check_bf16(wpe, "wpe");
+  check_bf16(w, "weight");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kLong && idx.dim() == 2,
+              "embed_layernorm: idx must be a (B, T) int64 GPU tensor");
+  TORCH_CHECK(wte.dim() == 2 && wpe.dim() == 2 && wte.size(1) == wpe.size(1),
+              "embed_layernorm: wte (V, C) and wpe (Tmax, C) must share C");
+  const int T = idx.size(1);
+  TORCH_CHECK(T <= wpe.size(0), "embed_layernorm: sequence longer than the position table");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(wte.device());
+  auto ic = idx.contiguous();
+  const int C = wte.size(1);
+  const int rows = ic.numel();
+  auto opts = wte.options();
+  auto y = at::empty({idx.size(0), T, C}, opts), sum = at::empty({idx.size(0), T, C}, opts);
+  auto fopts = opts.dtype(at::kFloat);
+  auto mean = at::empty({rows}, fopts), rstd = at::empty({rows}, fopts);
+  const void* bp = nullptr;
+  Tensor bc;
+  if (b.has_value() && b->defined()) {
+    check_bf16(*b, "bias");
+    bc = b->contiguous();
+    bp = bc.data_ptr();
+  }
+  auto wtec = wte.contiguous(), wpec = wpe.contiguous();
+  check_launch(orion_layernorm_fwd(wtec.data_ptr(), w.contiguous().data_ptr(), bp, y.data_ptr(),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, C,
+                                   (float)eps, wpec.data_ptr(), sum.data_ptr(), nullptr,
+                                   cur_stream(), ic.data_ptr<int64_t>(), T),
+               "embed_layernorm_fwd");
+  return {sum, y, mean, rstd};
+}
+
+// out[idx[i]] += dx[i] (fp32 atomics); out: the (V, C) fp32 table gradient
+void embed_scatter_add_(const Tensor& dx, const Tensor& idx, Tensor out) {
+  check_bf16(dx, "dx");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kLong, "idx must be int64 on the GPU");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 2,
+              "out must be a contiguous (V, C) float32 GPU tensor");
+  const int C = out.size(1);
+  TORCH_CHECK(dx.numel() == idx.numel() * C, "embed_scatter_add: dx must be (N, C) for N ids");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dx.device());
+  auto dxc = dx.contiguous(), ic = idx.contiguous();
+  check_launch(orion_embed_scatter_add(dxc.data_ptr(), ic.data_ptr<int64_t>(), out.data_ptr<float>(),
+                                       ic.numel(), C, cur_stream()),
+               "embed_scatter_add_");
+}
+
+// out (n) = sum over the leading dim of x (B, ...): fp32 or bf16 out (a gradient-arena slice)
+void batch_sum_(const Tensor& x, Tensor out) {
+  check_bf16(x, "x");
+  const long n = x.numel() / x.size(0);
+  TORCH_CHECK(has_out(out, n, "out"), "batch_sum_: out required");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto xc = x.contiguous();
+  check_launch(orion_batch_sum(xc.data_ptr(), out.data_ptr(), x.size(0), n, is_f32(out), cur_stream()),
+               "batch_sum_");
 }
 
 std::tuple<Tensor, Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x,
@@ -703,6 +770,9 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
 TORCH_LIBRARY(orion_amd, m) {
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias, Tensor? dres=None, bool want_dx_colsum=False, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, Tensor(c!)? dxs_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("embed_layernorm_fwd(Tensor idx, Tensor wte, Tensor wpe, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("embed_scatter_add_(Tensor dx, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("batch_sum_(Tensor x, Tensor(a!) out) -> ()");
   m.def("add_layernorm_fwd(Tensor x, Tensor r, Tensor w, Tensor? b, float eps, Tensor? rbias=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor x, Tensor? b) -> Tensor");
   m.def("bias_gelu_bwd(Tensor dy, Tensor x, Tensor? b, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");
@@ -732,6 +802,9 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("add_layernorm_fwd", &add_layernorm_fwd);
+  m.impl("embed_layernorm_fwd", &embed_layernorm_fwd);
+  m.impl("embed_scatter_add_", &embed_scatter_add_);
+  m.impl("batch_sum_", &batch_sum_);
   m.impl("bias_gelu_fwd", &bias_gelu_fwd);
   m.impl("bias_gelu_bwd", &bias_gelu_bwd);
   m.impl("colsum", &colsum);

@@ -36,11 +36,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
     int rows, int C, float eps, const bf16_t* __restrict__ res, bf16_t* __restrict__ sum_out,
-    const bf16_t* __restrict__ rbias) {
+    const bf16_t* __restrict__ rbias, const int64_t* __restrict__ idx, int T) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const bf16_t* xr = x + (size_t)row * C;
+  // idx: embedding gather -- x is the token table (row idx[row]) and res the position table
+  // (row row % T), so s = wte[idx] + wpe[t] is formed, returned and normalised in one pass
+  const bf16_t* xr = x + (size_t)(idx ? idx[row] : row) * C;
+  const size_t rrow = idx ? (size_t)(row % T) : (size_t)row;
   float v[ITERS][VEC];
   float s = 0.f;
 #pragma unroll
@@ -50,7 +53,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
       load_vec<VEC>(xr + c, v[i]);
       if (res) {  // fused residual add: s = x + r is both returned and normalised
         float rv[VEC];
-        load_vec<VEC>(res + (size_t)row * C + c, rv);
+        load_vec<VEC>(res + rrow * C + c, rv);
         if (rbias) {  // the branch's output-projection bias, added here instead of in the GEMM
           float bv[VEC];
           load_vec<VEC>(rbias + c, bv);
@@ -355,7 +358,7 @@ int orion_ln_max_cols() { return 2048; }
 
 int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
                         float* rstd, int rows, int C, float eps, const void* res, void* sum_out,
-                        const void* rbias, hipStream_t st) {
+                        const void* rbias, hipStream_t st, const int64_t* idx, int T) {
   int vec, it;
   if (!ln_pick(C, &vec, &it)) return -1;
   dim3 grid((rows + 3) / 4), block(256);
@@ -364,17 +367,17 @@ int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, fl
   auto R = (const bf16_t*)res; auto S = (bf16_t*)sum_out; auto RB = (const bf16_t*)rbias;
   if (vec == 8) {
     switch (it) {
-      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
-      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
-      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
-      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
     }
   } else {
     switch (it) {
-      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
-      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
-      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
-      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB); break;
+      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
     }
   }
   return (int)hipGetLastError();

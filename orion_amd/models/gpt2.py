@@ -156,18 +156,22 @@ class GPT(nn.Module):
     def forward(self, idx, targets=None):
         B, T = idx.shape
         assert T <= self.config.block_size, f"sequence {T} > block_size {self.config.block_size}"
-        tok = self.transformer.wte(idx)
-        pos = self.transformer.wpe.weight[:T]
-        x = ops.add_broadcast(tok, pos)
+        blocks = self.transformer.h
         if self.config.dropout and self.training:
+            tok = self.transformer.wte(idx)
+            x = ops.add_broadcast(tok, self.transformer.wpe.weight[:T])
             x = F.dropout(x, self.config.dropout)
+            h = blocks[0].ln_1(x)
+        else:
+            # token + position embedding and block 0's ln_1 in one op (ops/embedding.py)
+            ln = blocks[0].ln_1
+            x, h = ops.embed_layer_norm(idx, self.transformer.wte.weight, self.transformer.wpe.weight,
+                                        ln.weight, ln.bias)
         # Residual stream with every "x = x + branch; h = LN(x)" pair fused into one kernel
         # (forward and backward): block i's second add feeds block i+1's ln_1 (ln_f at the end).
         # The branch output-projection biases are folded into the same kernel
         # (forward: added before the residual sum; backward: their gradient is a
         # column sum of the residual-stream gradient the kernel already holds).
-        blocks = self.transformer.h
-        h = blocks[0].ln_1(x)
         for i, block in enumerate(blocks):
             a = block.attn(h, fuse_out_bias=True)
             x, h = ops.add_layer_norm(x, a, block.ln_2.weight, block.ln_2.bias,

@@ -145,6 +145,18 @@ def swiglu(gate_up):
     return ref.swiglu(gate, up)
 
 
+def embed_layer_norm(idx, wte, wpe, weight, bias, eps=1e-5):
+    """GPT-2's input: (x, h) = (wte[idx] + wpe[:T], LayerNorm(x)) for idx (B, T).  On the GPU
+    one kernel forward; backward writes the token-table gradient straight into its (tied)
+    gradient-arena slice (ops/embedding.py)."""
+    b = _gpu(wte)
+    if b == "hip" and wte.shape[1] % 8 == 0 and wte.shape[1] <= 2048:
+        from .embedding import embed_layer_norm_hip
+        return embed_layer_norm_hip(idx, wte, wpe, weight, bias, eps)
+    x = add_broadcast(F.embedding(idx, wte), wpe[:idx.shape[1]])
+    return x, layer_norm(x, weight, bias, eps)
+
+
 def add_broadcast(x, pos):
     """x (B, T, C) + pos (T, C); kept as one op so the GPU path is one kernel."""
     return x + pos.to(x.dtype)
@@ -230,6 +242,6 @@ def linear_cross_entropy(x, weight, targets, ignore_index=-1):
 
 __all__ = [
     "set_backend", "backend", "ext_available", "load_ext",
-    "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "rope",
+    "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm", "rope",
     "attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "linear_cross_entropy",
 ]

@@ -1,0 +1,98 @@
+"""Token + position embedding fused with the first LayerNorm (GPT-2), on the HIP kernels.
+
+Forward (one kernel, csrc/layernorm.hip in gather mode): s = wte[idx] + wpe[t] is formed,
+returned (the residual stream) and normalised; it replaces an embedding gather, a
+broadcast add and a LayerNorm pass.
+
+Backward: the LayerNorm backward folds the residual-stream gradient into dx (as for every
+other add+LayerNorm), then
+  * wpe: the column sum of dx over the batch, written into wpe's gradient-arena slice;
+  * wte: dx added row by row into the token table's fp32 arena slice with fp32 atomics
+    (csrc/embedding.hip).  The table is tied to the LM head, whose weight gradient was
+    written into the same slice at the start of the backward; the sink expects both
+    producers before it reports the parameter to the data-parallel reducer
+    (ops/grad_sink.py).  Deterministic mode and gradient-accumulation steps whose slice
+    cannot be written directly use the sort-based dense embedding backward.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import C
+from .determinism import deterministic
+from .grad_sink import sink_of
+from .layernorm import _bf16, _claim, _grad, _notify, _unless, _view
+
+
+def _dense_table_grad(dx2, idx, V):
+    return torch.ops.aten.embedding_dense_backward(dx2, idx.reshape(-1), V, -1, False)
+
+
+class _EmbedLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe, w, b, eps):
+        s, y, mean, rstd = C().embed_layernorm_fwd(idx, _bf16(wte), _bf16(wpe), _bf16(w), _bf16(b),
+                                                   float(eps))
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(idx, s, w, mean, rstd)
+        ctx.has_bias = b is not None
+        ctx.b_dtype = None if b is None else b.dtype
+        ctx.params = (w, b)
+        ctx.tables = (wte, wpe)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        idx, s, w, mean, rstd = ctx.saved_tensors
+        wte, wpe = ctx.tables
+        B, T, Cc = s.shape
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dres = None if ds is None else ds.contiguous()
+        sw, sb = _claim(ctx.params)
+        dx, dw, db, _ = C().layernorm_bwd(dy.contiguous(), s, _bf16(w), mean, rstd, ctx.has_bias,
+                                          dres, False, _view(sw), _view(sb))
+        _notify(sw, sb)
+        dw, db = _unless(dw, sw), _unless(db, sb)
+        dx2 = dx.view(B * T, Cc)
+
+        # position table: column sums of dx over the batch into rows 0..T-1
+        dwpe = None
+        if ctx.needs_input_grad[2]:
+            (spe,) = _claim((wpe,))
+            if spe is not None:
+                view = spe.view.view(-1, Cc)
+                C().batch_sum_(dx.view(B, T * Cc), view[:T].reshape(-1))
+                if view.shape[0] > T:  # positions this step did not use (slice not pre-zeroed)
+                    view[T:].zero_()
+                spe.notify()
+            else:
+                dwpe = torch.zeros_like(wpe, dtype=torch.float32)
+                dwpe[:T] = dx.float().sum(0)
+                dwpe = dwpe.to(wpe.dtype)
+
+        # token table (tied to the LM head)
+        dwte = None
+        if ctx.needs_input_grad[1]:
+            st = sink_of(wte)
+            if st is not None and st.view.dtype == torch.float32 and not deterministic():
+                acc = st.take()
+                if not acc:  # first producer of the step: the slice is not pre-zeroed
+                    st.view.zero_()
+                C().embed_scatter_add_(dx2, idx, st.view.view(-1, Cc))
+                st.notify()
+            elif st is not None:
+                g = _dense_table_grad(dx2, idx, wte.shape[0])
+                if st.take():
+                    st.view.view(-1, Cc).add_(g)
+                else:
+                    st.view.view(-1, Cc).copy_(g)
+                st.notify()
+            else:
+                dwte = _dense_table_grad(dx2, idx, wte.shape[0]).to(wte.dtype)
+        return (None, dwte, dwpe, _grad(dw, w.dtype),
+                (_grad(db, ctx.b_dtype) if ctx.has_bias else None), None)
+
+
+def embed_layer_norm_hip(idx, wte, wpe, weight, bias, eps=1e-5):
+    return _EmbedLayerNorm.apply(idx, wte, wpe, weight, bias, eps)

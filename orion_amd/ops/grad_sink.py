@@ -14,9 +14,12 @@ over micro-batches) -- and return ``None`` for the weight.  Because no
 ``AccumulateGrad`` runs, the sink then notifies the arena's gradient listeners (the
 data-parallel reducer's bucket counter) itself.
 
-Tied parameters (used by more than one module, e.g. GPT-2's ``wte`` / LM head) get no
-sink: their other contributions still arrive through ``AccumulateGrad``, and two
-producers would make the ordering of overwrite vs. accumulate ambiguous.
+Tied parameters (used by ``uses`` modules, e.g. GPT-2's ``wte`` = LM head) get a sink that
+expects ``uses`` producers per micro-step: the first write of a step overwrites, every
+later one accumulates (``take``), and the listeners fire only once all producers have
+reported (``notify``), so a data-parallel bucket is never launched between the LM head's
+contribution and the embedding's.  A producer without a sink (``AccumulateGrad``) is folded
+into the same slice by the arena and reported by the reducer's own hook.
 ``ORION_DIRECT_GRADS=0`` disables the mechanism.
 """
 from __future__ import annotations
@@ -30,13 +33,20 @@ ENABLED = os.environ.get("ORION_DIRECT_GRADS", "1") != "0"
 
 
 class GradSink:
-    __slots__ = ("view", "fresh", "_param", "_listeners", "__weakref__")
+    __slots__ = ("view", "fresh", "expect", "notes", "_param", "_listeners", "__weakref__")
 
-    def __init__(self, param: torch.Tensor, view: torch.Tensor, listeners: list):
+    def __init__(self, param: torch.Tensor, view: torch.Tensor, listeners: list, expect: int = 1):
         self.view = view            # the parameter's slice of the gradient arena, param-shaped
         self.fresh = True           # no write yet this step -> the next write may overwrite
+        self.expect = expect        # producers per micro-step (uses of a tied parameter)
+        self.notes = 0              # notify() calls since the step began
         self._param = weakref.ref(param)
         self._listeners = listeners  # shared with the owning arena
+
+    def reset(self):
+        """Start of an optimizer step (the arena's zero_grad)."""
+        self.fresh = True
+        self.notes = 0
 
     def take(self) -> bool:
         """Claim the slice for one write; returns True if the write must accumulate."""
@@ -45,16 +55,20 @@ class GradSink:
         return acc
 
     def notify(self):
+        self.notes += 1
+        if self.notes % self.expect:
+            return  # a tied parameter: another producer of this micro-step is still to come
         p = self._param()
         if p is not None:
             for cb in self._listeners:
                 cb(p)
 
 
-def attach(param: torch.Tensor, view: torch.Tensor, listeners: list) -> GradSink | None:
+def attach(param: torch.Tensor, view: torch.Tensor, listeners: list,
+           expect: int = 1) -> GradSink | None:
     if not ENABLED or view.dtype not in (torch.bfloat16, torch.float32) or not view.is_cuda:
         return None
-    sink = GradSink(param, view, listeners)
+    sink = GradSink(param, view, listeners, expect)
     param._orion_sink = sink
     return sink
 

@@ -106,15 +106,15 @@ class FlatArena:
                 self.init_fp32[s.offset: s.offset + s.numel].copy_(s.param.data.reshape(-1))
                 s.param.data = view
                 s.param.grad = self.grad_view(s).view_as(s.param) if self.bound else None
-        # direct-to-arena weight gradients (ops/grad_sink.py); tied parameters excluded
+        # direct-to-arena weight gradients (ops/grad_sink.py); a tied parameter's sink expects
+        # one producer per use
         self.grad_listeners: list = []
         self.sinks = []
         for s in slots:
-            if uses.get(id(s.param), 1) == 1:
-                sk = grad_sink.attach(s.param, self.grad_view(s).view_as(s.param),
-                                      self.grad_listeners)
-                if sk is not None:
-                    self.sinks.append(sk)
+            sk = grad_sink.attach(s.param, self.grad_view(s).view_as(s.param),
+                                  self.grad_listeners, expect=uses.get(id(s.param), 1))
+            if sk is not None:
+                self.sinks.append(sk)
         # zero_grad skips the slices of large sink-written weights: their first write of a
         # step overwrites (GradSink.fresh), so zeroing them first is a wasted HBM pass (27 GB
         # per step for Llama-7B's fp32 arena).  Everything else -- padding, small and tied
@@ -173,7 +173,7 @@ class FlatArena:
         elif self._zero_views:
             torch._foreach_zero_(self._zero_views)
         for sk in self.sinks:
-            sk.fresh = True
+            sk.reset()
 
     def finish_grads(self):
         """After the last backward of a step: zero the skipped sink slices that no kernel

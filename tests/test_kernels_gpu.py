@@ -609,3 +609,58 @@ def test_in_tree_gemm_path_matches_hipblaslt_in_the_model():
     assert abs(res[0][0] - res[1][0]) < 1e-2
     for n in res[0][1]:
         assert rel_err(res[1][1][n], res[0][1][n]) < 2e-2, n
+
+
+def test_embed_layer_norm_matches_reference():
+    """Fused token + position embedding + LayerNorm (one forward kernel; LayerNorm backward,
+    batch-summed position gradient and scatter-added token gradient) vs fp32 autograd of
+    the unfused ops, including repeated token ids; ragged T < block size."""
+    from orion_amd import ops
+    torch.manual_seed(0)
+    V, Tm, C, B, T = 1000, 96, 256, 3, 80
+    wte = (torch.randn(V, C, device=DEV) * 0.5).bfloat16().requires_grad_()
+    wpe = (torch.randn(Tm, C, device=DEV) * 0.5).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    idx = torch.randint(0, 50, (B, T), device=DEV)          # many repeats
+    ds, dh = torch.randn(B, T, C, device=DEV).bfloat16(), torch.randn(B, T, C, device=DEV).bfloat16()
+    x, h = ops.embed_layer_norm(idx, wte, wpe, w, b)
+    torch.autograd.backward((x, h), (ds, dh))
+    leaves = [t.detach().float().requires_grad_() for t in (wte, wpe, w, b)]
+    xr = leaves[0][idx] + leaves[1][:T]
+    hr = torch.nn.functional.layer_norm(xr, (C,), leaves[2], leaves[3], 1e-5)
+    torch.autograd.backward((xr, hr), (ds.float(), dh.float()))
+    assert rel_err(x, xr) < 1e-2 and rel_err(h, hr) < 2e-2
+    for name, got, want in zip(("wte", "wpe", "w", "b"), (wte.grad, wpe.grad, w.grad, b.grad),
+                               (t.grad for t in leaves)):
+        assert rel_err(got, want) < 2e-2, (name, rel_err(got, want))
+    assert float(wpe.grad[T:].float().abs().max()) == 0.0
+
+
+def test_tied_embedding_sink_reports_after_both_producers():
+    """GPT-2's tied wte / LM head: the LM head's weight gradient and the embedding's
+    scatter-add both land in the fp32 arena slice, the sink notifies the listeners once per
+    micro-step after the second producer, and the slice equals the AccumulateGrad path."""
+    from orion_amd.models.gpt2 import build_gpt2
+    from orion_amd.train.flat import FlatArena
+    torch.manual_seed(0)
+    m1, m2 = build_gpt2("gpt2-tiny").to(DEV), build_gpt2("gpt2-tiny").to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    a1, a2 = FlatArena(m1), FlatArena(m2)
+    a2.detach_sinks()
+    wte = m1.transformer.wte.weight
+    assert wte._orion_sink.expect == 2
+    seen = []
+    a1.grad_listeners.append(lambda p: seen.append(p is wte))
+    x = torch.randint(0, 64, (2, 128), device=DEV)      # repeated ids: atomics collide
+    for arena, model in ((a1, m1), (a2, m2)):
+        arena.zero_grad()
+        for _ in range(2):                               # two micro-steps
+            _, loss = model(x, x)
+            (loss / 2).backward()
+        arena.finish_grads()
+    assert seen.count(True) == 2
+    s = next(s for s in a1.slots if s.param is wte)
+    g1, g2 = (a.grads[s.offset:s.offset + s.numel] for a in (a1, a2))
+    assert rel_err(g1, g2) < 1e-2
+    assert rel_err(a1.grads, a2.grads) < 1e-2
