@@ -389,12 +389,56 @@ int orion_layernorm_bwd_blocks(int rows) {
   return nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
 }
 
+template <int VEC, int ITERS>
+static int ln_bwd_resident(size_t lds) {
+  static int per_cu = 0;
+  if (!per_cu) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ln_bwd_kernel<VEC, ITERS>, 256, lds) != hipSuccess || n < 1)
+      n = 1;
+    per_cu = n;
+  }
+  return per_cu;
+}
+
+static int ln_bwd_grid(int rows, int vec, int it, size_t lds) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  }
+  int per_cu = 1;
+  if (vec == 8) {
+    switch (it) {
+      case 1: per_cu = ln_bwd_resident<8, 1>(lds); break;
+      case 2: per_cu = ln_bwd_resident<8, 2>(lds); break;
+      case 3: per_cu = ln_bwd_resident<8, 3>(lds); break;
+      default: per_cu = ln_bwd_resident<8, 4>(lds); break;
+    }
+  } else {
+    switch (it) {
+      case 1: per_cu = ln_bwd_resident<4, 1>(lds); break;
+      case 2: per_cu = ln_bwd_resident<4, 2>(lds); break;
+      case 3: per_cu = ln_bwd_resident<4, 3>(lds); break;
+      default: per_cu = ln_bwd_resident<4, 4>(lds); break;
+    }
+  }
+  const int cap = orion_layernorm_bwd_blocks(rows);
+  const int one_round = per_cu * cus;
+  return one_round < cap ? one_round : cap;
+}
+
 int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
                         const float* rstd, void* dx, void* dw, void* db, float* part, int rows,
                         int C, const void* dres, void* drbias, int grad_f32, hipStream_t st) {
   int vec, it;
   if (!ln_pick(C, &vec, &it, /*exact_fit=*/true)) return -1;
-  const int nb = orion_layernorm_bwd_blocks(rows);
+  // One resident round of workgroups: the kernel strides over its rows, so a grid larger
+  // than what fits at once leaves a partial second round (at 152 VGPRs three 4-wave
+  // workgroups fit per CU: 1024 workgroups ran as 768 + 256).  The scratch is sized for
+  // orion_layernorm_bwd_blocks(rows) >= nb.
+  const int nb = ln_bwd_grid(rows, vec, it, (size_t)4 * C * sizeof(float));
   const int rpb = (rows + nb - 1) / nb;
   float* pdw = dw ? part : nullptr;
   float* pdb = db ? part + (size_t)nb * C : nullptr;

@@ -63,54 +63,69 @@ __global__ __launch_bounds__(XT, (XT == 512 ? 4 : 2)) void xent_fwd_bwd_kernel(
     bf16_t* __restrict__ logits, const int64_t* __restrict__ targets, float* __restrict__ losses,
     const float* __restrict__ inv_n, int V, long ignore) {
   constexpr int XW = XT / 64;
+  constexpr float L2E = 1.4426950408889634f;
   __shared__ float red[XW];
   const long row = blockIdx.x;
   bf16_t* lr = logits + row * (long)V;
   const int V8 = V >> 3;
   bf16x8 v[CH];
+  // pass 1: row max (max3 chains; this file builds with -fno-honor-nans, so fmaxf needs no
+  // canonicalising max per operand)
   float m = -INFINITY;
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = k * XT + threadIdx.x;
     if (c < V8) {
       v[k] = *reinterpret_cast<const bf16x8*>(lr + c * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m = fmaxf(m, bf2f(v[k][j]));
+      float a = fmaxf(fmaxf(bf2f(v[k][0]), bf2f(v[k][1])), bf2f(v[k][2]));
+      a = fmaxf(fmaxf(a, bf2f(v[k][3])), bf2f(v[k][4]));
+      a = fmaxf(fmaxf(a, bf2f(v[k][5])), bf2f(v[k][6]));
+      m = fmaxf(fmaxf(m, a), bf2f(v[k][7]));
     }
   }
   m = block_max<XW>(m, red);
-  float s = 0.f;
+  // pass 2: e = exp(x - m) as one fma + v_exp (base 2), kept in the registers as bf16 (the
+  // output is bf16 anyway) so pass 3 does not recompute it; four sum chains
+  const float m2 = m * L2E;
+  const long tgt = targets[row];
+  const bool valid = tgt != ignore;
+  // the thread whose 16-byte chunks hold the target logit owns the loss (one scalar
+  // re-read of that logit; a per-element compare against the target would cost a select
+  // per logit)
+  const bool owner = valid && (int)((tgt >> 3) % XT) == (int)threadIdx.x;
+  const float xt = owner ? bf2f(lr[tgt]) : 0.f;
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = k * XT + threadIdx.x;
     if (c < V8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += __expf(bf2f(v[k][j]) - m);
+      for (int j = 0; j < 8; ++j) {
+        const float e = __builtin_amdgcn_exp2f(fmaf(bf2f(v[k][j]), L2E, -m2));
+        s4[j & 3] += e;
+        v[k][j] = f2bf(e);
+      }
     }
   }
-  s = block_sum<XW>(s, red);
-  const long tgt = targets[row];
-  const bool valid = tgt != ignore;
+  const float s = block_sum<XW>((s4[0] + s4[1]) + (s4[2] + s4[3]), red);
   const float lse = m + __logf(s);
   const float scale = valid ? inv_n[0] : 0.f;
-  const float inv_s = 1.f / s;
+  const float f = scale / s;
   if (!valid && threadIdx.x == 0) losses[row] = 0.f;
+  // pass 3: dlogits = (softmax - onehot) / n_valid in place
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = k * XT + threadIdx.x;
     if (c < V8) {
       bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float p = __expf(bf2f(v[k][j]) - m) * inv_s;
-        if (c * 8 + j == tgt) {  // the owner of the target logit writes the row loss
-          p -= 1.f;
-          losses[row] = lse - bf2f(v[k][j]);
-        }
-        o[j] = f2bf(p * scale);
-      }
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(v[k][j]) * f);
       *reinterpret_cast<bf16x8*>(lr + c * 8) = o;
     }
+  }
+  if (owner) {  // the target's own term (after this thread's store of its chunk)
+    lr[tgt] = f2bf(__builtin_amdgcn_exp2f(fmaf(xt, L2E, -m2)) * f - scale);
+    losses[row] = lse - xt;
   }
 }
 

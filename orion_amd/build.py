@@ -43,7 +43,8 @@ def _torch_paths():
 
 # per-source extra flags (see the comment at the top of each file)
 FILE_FLAGS = {"attn_fwd.hip": ["-fno-honor-nans", "-fno-slp-vectorize"],
-              "attn_bwd_split.hip": ["-fno-honor-nans", "-fno-slp-vectorize"]}
+              "attn_bwd_split.hip": ["-fno-honor-nans", "-fno-slp-vectorize"],
+              "xent.hip": ["-fno-honor-nans", "-fno-slp-vectorize"]}
 
 
 def _newest_header():
