@@ -95,4 +95,4 @@ class _EmbedLayerNorm(torch.autograd.Function):
 
 
 def embed_layer_norm_hip(idx, wte, wpe, weight, bias, eps=1e-5):
-    return _EmbedLayerNorm.apply(idx, wte, wpe, weight, bias, eps)
+    return _EmbedLayerNorm.apply(idx.long(), wte, wpe, weight, bias, eps)

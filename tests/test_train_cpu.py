@@ -111,3 +111,27 @@ def test_fp32_grad_arena_for_bf16_params_folds_accumulate_grad():
         assert s.param.grad is None, s.name
         got = arena.grads[s.offset:s.offset + s.numel].view(s.param.shape)
         assert torch.allclose(got, ref_acc[s.name], atol=1e-6, rtol=1e-5), s.name
+
+
+def test_embed_layer_norm_cpu_path_matches_unfused():
+    """ops.embed_layer_norm on the CPU (the reference path the GPU kernel is tested against):
+    x = wte[idx] + wpe[:T], h = LayerNorm(x), gradients through both outputs."""
+    import torch
+    from orion_amd import ops
+    torch.manual_seed(0)
+    V, Tm, C, B, T = 50, 16, 32, 2, 12
+    wte, wpe = torch.randn(V, C, requires_grad=True), torch.randn(Tm, C, requires_grad=True)
+    w, b = torch.randn(C, requires_grad=True), torch.randn(C, requires_grad=True)
+    idx = torch.randint(0, V, (B, T))
+    x, h = ops.embed_layer_norm(idx, wte, wpe, w, b)
+    (x.sum() + (h * h).sum()).backward()
+    g = [t.grad.clone() for t in (wte, wpe, w, b)]
+    for t in (wte, wpe, w, b):
+        t.grad = None
+    x2 = wte[idx] + wpe[:T]
+    h2 = torch.nn.functional.layer_norm(x2, (C,), w, b, 1e-5)
+    (x2.sum() + (h2 * h2).sum()).backward()
+    assert torch.allclose(x, x2) and torch.allclose(h, h2, atol=1e-5)
+    for a, t in zip(g, (wte, wpe, w, b)):
+        assert torch.allclose(a, t.grad, atol=1e-4)
+    assert float(g[1][T:].abs().max()) == 0.0
