@@ -14,12 +14,14 @@ over micro-batches) -- and return ``None`` for the weight.  Because no
 ``AccumulateGrad`` runs, the sink then notifies the arena's gradient listeners (the
 data-parallel reducer's bucket counter) itself.
 
-Tied parameters (used by ``uses`` modules, e.g. GPT-2's ``wte`` = LM head) get a sink that
-expects ``uses`` producers per micro-step: the first write of a step overwrites, every
-later one accumulates (``take``), and the listeners fire only once all producers have
-reported (``notify``), so a data-parallel bucket is never launched between the LM head's
-contribution and the embedding's.  A producer without a sink (``AccumulateGrad``) is folded
-into the same slice by the arena and reported by the reducer's own hook.
+Tied parameters (used by ``uses`` > 1 modules, e.g. GPT-2's ``wte`` = LM head) get a sink
+too: the first write of a step overwrites, every later one accumulates (``take``).  Their
+``notify`` reports nothing: how many producers of a micro-step write through the sink
+depends on the graph (the GPT-2 input op does; a dropout path's plain embedding goes
+through ``AccumulateGrad`` and the arena's fold hook), so the parameter is reported by its
+post-accumulate-grad hook, which autograd runs once per backward after the LAST use's
+contribution -- a data-parallel bucket is never launched between the LM head's and the
+embedding's writes.
 ``ORION_DIRECT_GRADS=0`` disables the mechanism.
 """
 from __future__ import annotations
@@ -56,8 +58,8 @@ class GradSink:
 
     def notify(self):
         self.notes += 1
-        if self.notes % self.expect:
-            return  # a tied parameter: another producer of this micro-step is still to come
+        if self.expect > 1:
+            return  # tied: reported by the parameter's post-accumulate hook (module docstring)
         p = self._param()
         if p is not None:
             for cb in self._listeners:

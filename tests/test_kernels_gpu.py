@@ -639,8 +639,9 @@ def test_embed_layer_norm_matches_reference():
 
 def test_tied_embedding_sink_reports_after_both_producers():
     """GPT-2's tied wte / LM head: the LM head's weight gradient and the embedding's
-    scatter-add both land in the fp32 arena slice, the sink notifies the listeners once per
-    micro-step after the second producer, and the slice equals the AccumulateGrad path."""
+    scatter-add both land in the fp32 arena slice; the sink itself reports nothing (its
+    listeners never see wte), the parameter's post-accumulate hook fires once per micro-step
+    after both writes, and the slice equals the AccumulateGrad path."""
     from orion_amd.models.gpt2 import build_gpt2
     from orion_amd.train.flat import FlatArena
     torch.manual_seed(0)
@@ -650,8 +651,13 @@ def test_tied_embedding_sink_reports_after_both_producers():
     a2.detach_sinks()
     wte = m1.transformer.wte.weight
     assert wte._orion_sink.expect == 2
-    seen = []
+    seen, hooked = [], []
     a1.grad_listeners.append(lambda p: seen.append(p is wte))
+    s = next(s for s in a1.slots if s.param is wte)
+
+    def at_hook(p):  # the slice must already hold both contributions of this micro-step
+        hooked.append(float(a1.grads[s.offset:s.offset + s.numel].float().norm()))
+    wte.register_post_accumulate_grad_hook(at_hook)
     x = torch.randint(0, 64, (2, 128), device=DEV)      # repeated ids: atomics collide
     for arena, model in ((a1, m1), (a2, m2)):
         arena.zero_grad()
@@ -659,8 +665,8 @@ def test_tied_embedding_sink_reports_after_both_producers():
             _, loss = model(x, x)
             (loss / 2).backward()
         arena.finish_grads()
-    assert seen.count(True) == 2
-    s = next(s for s in a1.slots if s.param is wte)
+    assert seen.count(True) == 0
+    assert len(hooked) == 2 and hooked[1] > hooked[0] > 0
     g1, g2 = (a.grads[s.offset:s.offset + s.numel] for a in (a1, a2))
     assert rel_err(g1, g2) < 1e-2
     assert rel_err(a1.grads, a2.grads) < 1e-2
