@@ -55,7 +55,8 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=64)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="DDP gradient bucket size (default: 64 MB, 256 MB from 1B parameters up)")
     ap.add_argument("--no-tuned-gemms", action="store_true",
                     help="do not load the committed TunableOp GEMM table (orion_amd/tuning/)")
     ap.add_argument("--gemm-table", default=None, help="TunableOp table to load instead of the committed one")
@@ -131,7 +132,7 @@ def main():
         if world > 1:
             ddp_model = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[dev.index] if dev.type == "cuda" else None,
-                                                                  bucket_cap_mb=args.bucket_mb)
+                                                                  bucket_cap_mb=args.bucket_mb or 64.0)
         opt = torch.optim.AdamW(model.parameters(), lr=ocfg.learning_rate, betas=(0.9, 0.95),
                                 weight_decay=0.1, fused=True)
 

@@ -5,7 +5,7 @@ Design (MI355X-first, not a translation of any NCCL call pattern):
 * gradients live in ONE flat arena (``train/flat.py``) laid out in reverse
   module order, so a bucket is a contiguous slice of it: an all-reduce runs
   in place on the arena, no copy-in/copy-out and no per-parameter launches;
-* buckets default to 64 MB: a ring all-reduce on an 8-GPU xGMI node is bound
+* buckets default to 64 MB (256 MB from 1B parameters up, ``default_bucket_mb``): a ring all-reduce on an 8-GPU xGMI node is bound
   by per-link bandwidth (7 point-to-point links, ~153 GB/s each), and RCCL
   needs tens of MB per call to spread its channels over all links; fewer,
   larger collectives also mean fewer launches competing with backward;
@@ -36,9 +36,20 @@ import torch.distributed as dist
 from ..train.flat import FlatArena
 
 
+def default_bucket_mb(n_params: int) -> float:
+    """Bucket size for a model of ``n_params`` parameters.  64 MB for GPT-2-class models
+    (~8 buckets of the 0.5 GB fp32 arena: the first launches a few layers into backward);
+    256 MB from 1B parameters up (Llama-7B's 27 GB fp32 arena: ~105 collectives per step
+    instead of ~420, three per decoder layer), where per-call latency and RCCL's channel
+    ramp-up would otherwise eat into the xGMI link bandwidth."""
+    return 256.0 if n_params >= 1_000_000_000 else 64.0
+
+
 class GradBucketReducer:
-    def __init__(self, arena: FlatArena, bucket_mb: float = 64.0, group=None,
+    def __init__(self, arena: FlatArena, bucket_mb: float | None = None, group=None,
                  average: bool = True):
+        if bucket_mb is None or bucket_mb <= 0:
+            bucket_mb = default_bucket_mb(arena.numel)
         self.arena = arena
         self.group = group
         self.world = dist.get_world_size(group)

@@ -68,7 +68,7 @@ class Trainer:
     GRAPH_MAX_TOKENS = int(os.environ.get("ORION_GRAPH_MAX_TOKENS", 0))
 
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
-                 ddp: bool | None = None, bucket_mb: float = 64.0, arena_dtype=None,
+                 ddp: bool | None = None, bucket_mb: float | None = None, arena_dtype=None,
                  graph: bool = False, grad_dtype=None):
         self.model = model
         self.cfg = optim or OptimConfig()

@@ -173,3 +173,9 @@ def test_bench_spawns_its_own_ranks_on_cpu():
     assert rec["steps"] == 2 and rec["warmup"] == 1
     assert abs(rec["per_gpu"] * 2 - rec["value"]) / rec["value"] < 1e-3
     assert rec["allreduce_busbw_gbps"] is not None
+
+
+def test_default_bucket_size_by_model_size():
+    from orion_amd.parallel.ddp import default_bucket_mb
+    assert default_bucket_mb(124_000_000) == 64.0
+    assert default_bucket_mb(6_740_000_000) == 256.0

@@ -10,7 +10,7 @@ init_from, dataset, gradient_accumulation_steps, batch_size, block_size,
 n_layer, n_head, n_embd, dropout, bias, learning_rate, max_iters,
 weight_decay, beta1, beta2, grad_clip, decay_lr, warmup_iters,
 lr_decay_iters, min_lr) plus ``model`` (a preset: gpt2, gpt2-medium,
-llama2-7b, llama-tiny ...) and ``bucket_mb``.  Python config files are read
+llama2-7b, llama-tiny ...) and ``bucket_mb`` (0 = by model size, ``parallel.ddp.default_bucket_mb``).  Python config files are read
 for literal ``key = value`` assignments only (parsed with ``ast``; nothing is
 executed).  ``dataset`` names ``data/<dataset>/{train,val}.bin`` (uint16 token
 shards); if absent, synthetic tokens are used.
@@ -39,7 +39,7 @@ DEFAULTS = dict(
     model="gpt2", n_layer=12, n_head=12, n_embd=768, dropout=0.0, bias=True,
     learning_rate=6e-4, max_iters=600000, weight_decay=1e-1, beta1=0.9, beta2=0.95,
     grad_clip=1.0, decay_lr=True, warmup_iters=2000, lr_decay_iters=600000, min_lr=6e-5,
-    backend="nccl", device="cuda", dtype="bfloat16", seed=1337, bucket_mb=64.0,
+    backend="nccl", device="cuda", dtype="bfloat16", seed=1337, bucket_mb=0.0,
     data_root="data",
     # tracing: profile_steps > 0 records that many steps, starting at
     # profile_start, with torch.profiler and writes a Chrome trace to out_dir
