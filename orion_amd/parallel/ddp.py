@@ -5,7 +5,8 @@ Design (MI355X-first, not a translation of any NCCL call pattern):
 * gradients live in ONE flat arena (``train/flat.py``) laid out in reverse
   module order, so a bucket is a contiguous slice of it: an all-reduce runs
   in place on the arena, no copy-in/copy-out and no per-parameter launches;
-* buckets default to 64 MB (256 MB from 1B parameters up, ``default_bucket_mb``): a ring all-reduce on an 8-GPU xGMI node is bound
+* buckets default to 64 MB (256 MB from 1B parameters up, ``default_bucket_mb``):
+  a ring all-reduce on an 8-GPU xGMI node is bound
   by per-link bandwidth (7 point-to-point links, ~153 GB/s each), and RCCL
   needs tens of MB per call to spread its channels over all links; fewer,
   larger collectives also mean fewer launches competing with backward;

@@ -10,7 +10,8 @@ init_from, dataset, gradient_accumulation_steps, batch_size, block_size,
 n_layer, n_head, n_embd, dropout, bias, learning_rate, max_iters,
 weight_decay, beta1, beta2, grad_clip, decay_lr, warmup_iters,
 lr_decay_iters, min_lr) plus ``model`` (a preset: gpt2, gpt2-medium,
-llama2-7b, llama-tiny ...) and ``bucket_mb`` (0 = by model size, ``parallel.ddp.default_bucket_mb``).  Python config files are read
+llama2-7b, llama-tiny ...) and ``bucket_mb``
+(0 = by model size, ``parallel.ddp.default_bucket_mb``).  Python config files are read
 for literal ``key = value`` assignments only (parsed with ``ast``; nothing is
 executed).  ``dataset`` names ``data/<dataset>/{train,val}.bin`` (uint16 token
 shards); if absent, synthetic tokens are used.
