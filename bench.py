@@ -88,10 +88,7 @@ def main():
         dev = launch.device_for(local_rank, local_world, args.dist_backend)
         torch.cuda.set_device(dev)
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.dist_backend)
+        launch.init_process_group(args.dist_backend, dev if args.dist_backend == "nccl" else None)
     n_tuned = 0
     # TunableOp's table is not applied under HIP-graph capture (solutions chosen by index
     # went wrong on replay in testing); graph runs use hipBLASLt's default heuristics

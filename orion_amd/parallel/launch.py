@@ -114,3 +114,24 @@ def device_for(local_rank: int, local_world: int, backend: str):
         return torch.device("cuda", local_rank)
     # gloo rehearsal: ranks may share a device (or run on the CPU)
     return torch.device("cuda", local_rank % n) if n else torch.device("cpu")
+
+
+def init_process_group(backend: str, dev=None):
+    """``torch.distributed`` init for a rank.  RCCL (``nccl``): eager communicator setup on
+    this rank's device, and collectives on a HIGH-priority HIP stream, so a bucket's
+    all-reduce is dispatched ahead of the backward GEMM workgroups queued on the compute
+    stream instead of behind them (the overlap the bucketed reducer relies on).
+    ``ORION_RCCL_HIGH_PRIO=0`` keeps the default-priority stream."""
+    import torch.distributed as dist
+    if backend != "nccl":
+        dist.init_process_group(backend)
+        return
+    opts = None
+    if os.environ.get("ORION_RCCL_HIGH_PRIO", "1") != "0":
+        try:
+            from torch.distributed import ProcessGroupNCCL
+            opts = ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+        except (ImportError, AttributeError):
+            opts = None
+    dist.init_process_group("nccl", device_id=dev, pg_options=opts)

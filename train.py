@@ -101,7 +101,8 @@ def main(argv=None):
         rank, local_rank, world = (int(os.environ[k]) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"))
         if cfg["device"].startswith("cuda"):
             torch.cuda.set_device(local_rank)
-            dist.init_process_group(cfg["backend"], device_id=torch.device("cuda", local_rank))
+            from orion_amd.parallel.launch import init_process_group
+            init_process_group(cfg["backend"], torch.device("cuda", local_rank))
         else:
             dist.init_process_group("gloo")
     master = rank == 0
