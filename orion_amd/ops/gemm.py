@@ -95,6 +95,13 @@ def linear_dgrad(dy, w):
         return C().gemm(dy, w, True, EPI_STORE, None, None)[0]
     return dy @ w
 
+# Order of a linear layer's two backward GEMMs.  Both read dY; the input gradient dX is
+# consumed by the very next backward kernel (LayerNorm / GELU / attention backward), the
+# weight gradient by nothing until the optimizer.  ORION_WGRAD_FIRST=1 issues the weight
+# gradient first, so dX is written right before its consumer reads it and is still in the
+# 256 MB Infinity Cache (the weight gradient's operand streaming would evict it otherwise).
+WGRAD_FIRST = os.environ.get("ORION_WGRAD_FIRST", "0") == "1"
+
 _FORCE = os.environ.get("ORION_WGRAD_SPLITS")
 _IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/gemm_phased.hip) | "blas" | "bmm"
 

@@ -6,7 +6,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
-from .gemm import linear_dgrad, linear_fwd, wgrad, wgrad_into
+from .gemm import WGRAD_FIRST, linear_dgrad, linear_fwd, wgrad, wgrad_into
 from .grad_sink import claim, sink_of
 
 
@@ -128,7 +128,10 @@ class _Linear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        bias_grad = ctx.has_bias and ctx.needs_input_grad[2]
+        if bias_grad and WGRAD_FIRST:  # dY was just written by the previous kernel: sum it now
+            db = _Linear._bias_grad(ctx, dy2)
+        if ctx.needs_input_grad[0] and not WGRAD_FIRST:
             dx = linear_dgrad(dy2, w).view(x.shape)
         if ctx.needs_input_grad[1]:
             sink = ctx.sink
@@ -137,13 +140,20 @@ class _Linear(torch.autograd.Function):
                 sink.notify()
             else:
                 dw = wgrad(dy2, x.reshape(-1, x.shape[-1]))
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            (sb,) = _claim((ctx.bias,))
-            db = C().colsum(dy2.contiguous(), _view(sb))
-            if sb is not None:  # written into the arena; never hand the slice back to autograd
-                db = None
-            _notify(sb)
+        if ctx.needs_input_grad[0] and WGRAD_FIRST:
+            dx = linear_dgrad(dy2, w).view(x.shape)
+        if bias_grad and not WGRAD_FIRST:
+            db = _Linear._bias_grad(ctx, dy2)
         return dx, dw, db
+
+    @staticmethod
+    def _bias_grad(ctx, dy2):
+        (sb,) = _claim((ctx.bias,))
+        db = C().colsum(dy2.contiguous(), _view(sb))
+        if sb is not None:  # written into the arena; never hand the slice back to autograd
+            db = None
+        _notify(sb)
+        return db
 
 
 def linear_hip(x, weight, bias=None):

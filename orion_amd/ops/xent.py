@@ -10,7 +10,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import C
-from .gemm import linear_dgrad, linear_fwd, wgrad, wgrad_into
+from .gemm import WGRAD_FIRST, linear_dgrad, linear_fwd, wgrad, wgrad_into
 from .grad_sink import sink_of
 
 
@@ -28,7 +28,7 @@ class _LinearXent(torch.autograd.Function):
         x, w, dl = ctx.saved_tensors
         s = g.detach().float().reshape(1).contiguous()
         dx = dw = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and not WGRAD_FIRST:
             dx = linear_dgrad(dl, w)
             C().scale_(dx, s)
         if ctx.needs_input_grad[1]:
@@ -38,6 +38,9 @@ class _LinearXent(torch.autograd.Function):
                 sink.notify()
             else:
                 dw = wgrad(dl, x, s)
+        if ctx.needs_input_grad[0] and WGRAD_FIRST:
+            dx = linear_dgrad(dl, w)
+            C().scale_(dx, s)
         return dx, dw, None, None
 
 
