@@ -52,7 +52,9 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=1024)
     # 64 x 1024 tokens per GPU per step: at dp8 that is 524,288 tokens per optimizer step,
     # the same global batch as nanoGPT's GPT-2-124M recipe (12 x 1024 x 40 = 491,520).
-    ap.add_argument("--micro-batch", type=int, default=64)
+    ap.add_argument("--micro-batch", type=int, default=None,
+                    help="sequences per micro-batch (default: 64 for GPT-2 presets; 16,384 tokens "
+                         "per micro-batch for Llama presets, i.e. 4 at seq 4096)")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
     ap.add_argument("--bucket-mb", type=float, default=None,
@@ -111,6 +113,8 @@ def main():
     with torch.device(dev):  # parameters are created (and initialised) on the GPU: 7B shapes included
         model = build_model(args.model, **ctx_kw)
     n_params = model.num_params()
+    if args.micro_batch is None:
+        args.micro_batch = 64 if is_gpt2 else max(1, 16384 // args.seq_len)
     B, T, A = args.micro_batch, args.seq_len, args.grad_accum
     # token ids below GPT-2's real vocabulary (50257); the padded embedding rows stay unused
     vocab = 50257 if is_gpt2 else model.config.vocab_size
