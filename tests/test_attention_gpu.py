@@ -162,3 +162,48 @@ def test_forward_kernel_variants_match_reference(env):
     lines = [ln for ln in r.stdout.splitlines() if "max err" in ln]
     assert len(lines) == 7, r.stdout
     assert all("bad rows 0 /" in ln for ln in lines), r.stdout
+
+
+_DELTA_MODE = r"""
+import math, os, sys, torch
+sys.path.insert(0, os.environ["ORION_REPO"])
+sys.path.insert(0, os.path.join(os.environ["ORION_REPO"], "tests"))
+from test_attention_gpu import SPLIT, _inputs, _ref, _run, rel_err
+for (B, T, Tk, Hq, Hkv, D, causal) in [(2, 320, 320, 4, 4, 64, True), (1, 256, 384, 8, 2, 128, True),
+                                      (2, 200, 200, 4, 2, 64, False)]:
+    q, k, v, do = _inputs(B, T, Tk, Hq, Hkv, D, seed=3)
+    _, dq, dk, dv = _run(q, k, v, do, causal, SPLIT)
+    _, wdq, wdk, wdv = _ref(q, k, v, do, causal)
+    errs = [rel_err(dq, wdq), rel_err(dk, wdk), rel_err(dv, wdv)]
+    assert max(errs) < 3e-2, (B, T, Tk, D, causal, errs)
+    torch.save((dq.cpu(), dk.cpu(), dv.cpu()), os.path.join(os.environ["OUT"], f"{T}_{Tk}_{D}.pt"))
+print("delta mode ok", os.environ.get("ORION_ATTN_DELTA", "kernel"))
+"""
+
+
+def test_split_backward_delta_modes_match(tmp_path):
+    """delta = rowsum(dO O) as its own pass (default) and fused into the dQ kernel
+    (ORION_ATTN_DELTA=fused): both vs the fp32 reference, and the two agree to fp32 rounding
+    of the delta sums.  The mode is read once per process: one child process each."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for mode in ("fused", "kernel"):
+        out = tmp_path / mode
+        out.mkdir()
+        env = {**os.environ, "ORION_REPO": root, "OUT": str(out)}
+        if mode == "fused":
+            env["ORION_ATTN_DELTA"] = "fused"
+        else:
+            env.pop("ORION_ATTN_DELTA", None)
+        r = subprocess.run([sys.executable, "-c", _DELTA_MODE], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        outs[mode] = out
+    for f in sorted(os.listdir(outs["fused"])):
+        a = torch.load(outs["fused"] / f, weights_only=True)
+        b = torch.load(outs["kernel"] / f, weights_only=True)
+        for x, y in zip(a, b):
+            assert rel_err(x, y) < 2e-3, f
