@@ -141,8 +141,11 @@ l1 = tr.step(xb)
 l0 = ref.step(xb)
 torch.cuda.synchronize()
 assert tr.reducer.launch_log == list(range(len(tr.reducer.buckets))), tr.reducer.launch_log
-assert torch.equal(tr.arena.grads, ref.arena.grads), (tr.arena.grads - ref.arena.grads).abs().max()
-assert torch.equal(tr.arena.params, ref.arena.params)
+# equal up to the order of the token-table backward's fp32 atomics (run-to-run rounding)
+gd = (tr.arena.grads - ref.arena.grads).abs().max()
+assert gd <= 1e-6 * ref.arena.grads.abs().max(), gd
+md = (tr.opt.master - ref.opt.master).abs().max()
+assert md <= 1e-6 * ref.opt.master.abs().max(), md
 print("RCCL one-rank ok", float(l1), float(l0), len(tr.reducer.buckets))
 dist.destroy_process_group()
 """
@@ -152,7 +155,8 @@ def test_rccl_one_rank_reducer_matches_local_step():
     """The real RCCL path on the one-GPU box: a world-size-1 ``nccl`` process group made by
     ``parallel.launch.init_process_group`` (high-priority collective stream), the bucketed
     reducer's async all-reduces issued from the backward hooks in bucket order, and the
-    step's gradients / weights bit-identical to the same step without a reducer."""
+    step's gradients / weights equal to the same step without a reducer (up to the
+    run-to-run rounding of the embedding backward's fp32 atomics)."""
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
