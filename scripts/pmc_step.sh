@@ -1,0 +1,28 @@
+#!/bin/bash
+# Whole-training-step PMC passes (each its own rocprofv3 run with --kernel-trace only):
+#   m: MFMA busy cycles, MFMA / VALU instruction counts, GPU-active cycles
+#   f: HBM-side fetch bytes (TCC FETCH_SIZE)      w: write bytes (TCC WRITE_SIZE)
+# over a 2-step GPT-2 bench, then the per-kernel-group table of scripts/pmc_step_summary.py.
+# usage: scripts/pmc_step.sh TAG [bench args]
+set -o pipefail
+cd "$(dirname "$0")/.."
+REPO=$(pwd)
+TAG=${1:-step}; shift
+ARGS=${*:-"--steps 1 --warmup 1"}
+OUT=$REPO/gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+cd /tmp || exit 1
+run() {
+  p=$1; shift
+  # shellcheck disable=SC2086
+  timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/$p" -o run \
+    -- python3 "$REPO/bench.py" $ARGS > "$OUT/$p.log" 2>&1 || { tail -20 "$OUT/$p.log"; return 1; }
+}
+run m SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE && \
+run f FETCH_SIZE GRBM_GUI_ACTIVE && \
+run w WRITE_SIZE GRBM_GUI_ACTIVE
+rc=$?
+cd "$REPO" || exit 1
+python3 scripts/pmc_step_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+exit $rc

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Per-kernel-group counters of a whole training step (scripts/pmc_step.sh output).
+
+For each kernel group (scripts/prof_summary.py's categories, GEMM kernels split by family):
+time from the kernel trace of the MFMA pass, MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES /
+(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) -- GRBM_GUI_ACTIVE comes summed over the 8 XCDs (it reads
+~15.7 per ns of kernel time at ~1.96 GHz) -- and HBM-side traffic (TCC FETCH_SIZE + WRITE_SIZE, KiB) as
+bytes and achieved bandwidth over the group's kernel time.  Counter passes come from separate
+runs of the same step; kernels are matched by dispatch order within each run.
+
+usage: python scripts/pmc_step_summary.py gpurun_out/pmc_TAG
+"""
+import collections
+import csv
+import glob
+import os
+import sys
+
+SIMDS = 256 * 4
+XCDS = 8
+
+
+def group(name):
+    n = name.lower()
+    if "gemm_phased" in n:
+        return "GEMM in-tree phased (weight gradients)"
+    if "cijk" in n or "gemm[" in n:
+        return "GEMM hipBLASLt (forward, input gradients)"
+    for key, g in (("attn_fwd", "attention forward"), ("attn_bwd_kv", "attention bwd dK/dV"),
+                   ("attn_bwd_dq", "attention bwd dQ"), ("attn_delta", "attention delta"),
+                   ("ln_fwd", "LayerNorm fwd"), ("ln_bwd", "LayerNorm bwd"),
+                   ("bias_gelu_fwd", "bias+GELU fwd"), ("bias_gelu_bwd", "bias+GELU bwd"),
+                   ("xent", "cross-entropy"), ("adamw", "AdamW"), ("colsum", "column sums"),
+                   ("slab_sum", "split-K slab sums")):
+        if key in n:
+            return g
+    return "other"
+
+
+def load(d, p):
+    """{dispatch index in run order: (kernel name, {counter: value}, duration ns)}"""
+    cc = glob.glob(os.path.join(d, p, "**", "*counter_collection.csv"), recursive=True)
+    kt = glob.glob(os.path.join(d, p, "**", "*kernel_trace.csv"), recursive=True)
+    if not cc:
+        return {}
+    dur = {}
+    if kt:
+        for r in csv.DictReader(open(kt[0])):
+            dur[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    per = collections.defaultdict(dict)
+    names = {}
+    for r in csv.DictReader(open(cc[0])):
+        i = int(r["Dispatch_Id"])
+        per[i][r["Counter_Name"]] = per[i].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        names[i] = r["Kernel_Name"]
+    return {k: (names[k], per[k], dur.get(k, 0)) for k in sorted(per)}
+
+
+def main():
+    d = sys.argv[1]
+    m, f, w = load(d, "m"), load(d, "f"), load(d, "w")
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    mk, fk, wk = list(m.values()), list(f.values()), list(w.values())
+    for i, (name, c, ns) in enumerate(mk):
+        g = agg[group(name)]
+        g["n"] += 1
+        g["ns"] += ns
+        g["mfma"] += c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        g["active"] += c.get("GRBM_GUI_ACTIVE", 0.0)
+        if i < len(fk) and fk[i][0] == name:
+            g["fetch"] += fk[i][1].get("FETCH_SIZE", 0.0) * 1024
+        if i < len(wk) and wk[i][0] == name:
+            g["write"] += wk[i][1].get("WRITE_SIZE", 0.0) * 1024
+    tot = sum(g["ns"] for g in agg.values())
+    print(f"{len(mk)} dispatches, {tot / 1e6:.2f} ms of kernels (2-step bench under the counter pass)")
+    print(f"{'group':44s} {'ms':>8s} {'%':>5s} {'MFMA util':>9s} {'L2-EA GB':>8s} {'TB/s':>6s}")
+    for k, g in sorted(agg.items(), key=lambda x: -x[1]["ns"]):
+        util = g["mfma"] / (g["active"] / XCDS * SIMDS) if g["active"] else 0.0
+        gb = (g["fetch"] + g["write"]) / 1e9
+        tbs = gb / (g["ns"] / 1e9) / 1e3 if g["ns"] else 0.0
+        print(f"{k:44s} {g['ns'] / 1e6:8.2f} {100 * g['ns'] / tot:5.1f} {100 * util:8.1f}% {gb:8.2f} {tbs:6.2f}")
+
+
+if __name__ == "__main__":
+    main()
