@@ -89,7 +89,13 @@ def main():
     else:
         dev = launch.device_for(local_rank, local_world, args.dist_backend)
         torch.cuda.set_device(dev)
+    rccl_log = None
     if world > 1:
+        if args.dist_backend == "nccl":
+            # RCCL's topology / channel INFO log of this rank goes to a file, summarised below
+            rccl_log = launch.rccl_debug_env(
+                os.environ.get("ORION_BENCH_LOGDIR", os.path.join(ROOT, "gpurun_out", "bench_logs")),
+                rank)
         launch.init_process_group(args.dist_backend, dev if args.dist_backend == "nccl" else None)
     n_tuned = 0
     # TunableOp's table is not applied under HIP-graph capture (solutions chosen by index
@@ -126,7 +132,8 @@ def main():
     ocfg = OptimConfig(warmup_iters=10, lr_decay_iters=10000)
     if args.impl == "native":
         trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb, graph=args.hip_graph and world == 1,
-                          grad_dtype=torch.float32 if args.grad_dtype == "fp32" else torch.bfloat16)
+                          grad_dtype=torch.float32 if args.grad_dtype == "fp32" else torch.bfloat16,
+                          ddp_timing=world > 1)
         step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
     else:
         ddp_model = model
@@ -182,10 +189,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     final_loss = float(loss)
-    busbw = None
-    if world > 1 and not args.no_busbw and args.impl == "native":
-        from orion_amd.parallel.busbw import allreduce_busbw
-        busbw = allreduce_busbw(trainer.arena.grads, iters=5)
+    busbw = ddp = rccl = None
+    if world > 1 and args.impl == "native":
+        # bucket timeline of the last timed step: launch -> complete per bucket, exposed tail
+        ddp = trainer.reducer.timing_report()
+        if ddp is not None:
+            t = torch.tensor([ddp["exposed_tail_ms"], ddp["comm_ms"]], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ddp["exposed_tail_ms_max_over_ranks"] = round(float(t[0]), 3)
+            ddp["comm_ms_max_over_ranks"] = round(float(t[1]), 3)
+        if not args.no_busbw:
+            from orion_amd.parallel.busbw import allreduce_busbw
+            busbw = allreduce_busbw(trainer.arena.grads, iters=5)
+        if rccl_log is not None:
+            from orion_amd.parallel.busbw import rccl_summary
+            rccl = rccl_summary(rccl_log)
 
     tokens = world * B * T * A * args.steps
     tok_s = tokens / elapsed
@@ -223,6 +241,8 @@ def main():
                            if dev.type == "cuda" else None),
             "dist_backend": args.dist_backend if world > 1 else None,
             "allreduce_busbw_gbps": busbw,
+            "ddp_buckets": ddp,
+            "rccl": rccl,
             "config": {"model": f"{args.model} ({n_params / 1e6:.1f}M params)",
                        "global_batch": B * A * world, "micro_batch": B, "grad_accum": A,
                        "seq_len": T, "tokens_per_step": B * T * A * world,

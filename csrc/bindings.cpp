@@ -19,8 +19,8 @@
 // launchers (csrc/*.hip)
 int orion_layernorm_fwd(const void*, const void*, const void*, void*, float*, float*, int, int,
                         float, const void*, void*, const void*, hipStream_t,
-                        const int64_t* idx = nullptr, int T = 0);
-int orion_embed_scatter_add(const void*, const int64_t*, float*, long, int, hipStream_t);
+                        const int64_t* idx = nullptr, int T = 0, long V = 0, int* err = nullptr);
+int orion_embed_scatter_add(const void*, const int64_t*, float*, long, int, long, int*, hipStream_t);
 int orion_batch_sum(const void*, void*, int, long, int, hipStream_t);
 int orion_layernorm_bwd_blocks(int rows);
 int orion_layernorm_bwd(const void*, const void*, const void*, const float*, const float*, void*,
@@ -65,6 +65,20 @@ using at::Tensor;
 
 hipStream_t cur_stream() {
   return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
+
+// one int per device, allocated on first use (before any graph capture: the first embedding
+// call of a process runs eagerly), zeroed once
+int* id_error_flag(int device) {
+  static int* flags[64] = {nullptr};
+  TORCH_CHECK(device >= 0 && device < 64, "device index out of range");
+  if (!flags[device]) {
+    int* p = nullptr;
+    TORCH_CHECK(hipMalloc(&p, sizeof(int)) == hipSuccess && hipMemset(p, 0, sizeof(int)) == hipSuccess,
+                "id_error_flag: allocation failed");
+    flags[device] = p;
+  }
+  return flags[device];
 }
 
 void check_launch(int rc, const char* what) {
@@ -190,7 +204,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> embed_layernorm_fwd(const Tensor& idx
   check_launch(orion_layernorm_fwd(wtec.data_ptr(), w.contiguous().data_ptr(), bp, y.data_ptr(),
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, C,
                                    (float)eps, wpec.data_ptr(), sum.data_ptr(), nullptr,
-                                   cur_stream(), ic.data_ptr<int64_t>(), T),
+                                   cur_stream(), ic.data_ptr<int64_t>(), T, wte.size(0),
+                                   id_error_flag(wte.device().index())),
                "embed_layernorm_fwd");
   return {sum, y, mean, rstd};
 }
@@ -206,8 +221,24 @@ void embed_scatter_add_(const Tensor& dx, const Tensor& idx, Tensor out) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(dx.device());
   auto dxc = dx.contiguous(), ic = idx.contiguous();
   check_launch(orion_embed_scatter_add(dxc.data_ptr(), ic.data_ptr<int64_t>(), out.data_ptr<float>(),
-                                       ic.numel(), C, cur_stream()),
+                                       ic.numel(), C, out.size(0),
+                                       id_error_flag(dx.device().index()), cur_stream()),
                "embed_scatter_add_");
+}
+
+// Token-id error flag of a device: nonzero once an embedding kernel saw an id outside its
+// table (the id was clamped / skipped, nothing outside the table was touched).  Reads the
+// flag (synchronises the current stream) and clears it.
+int64_t embed_id_error(int64_t device) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (int)device));
+  int* f = id_error_flag((int)device);
+  int v = 0;
+  auto st = cur_stream();
+  TORCH_CHECK(hipMemcpyAsync(&v, f, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                  hipMemsetAsync(f, 0, sizeof(int), st) == hipSuccess &&
+                  hipStreamSynchronize(st) == hipSuccess,
+              "embed_id_error: flag read failed");
+  return v;
 }
 
 // out (n) = sum over the leading dim of x (B, ...): fp32 or bf16 out (a gradient-arena slice)
@@ -772,6 +803,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, bool has_bias, Tensor? dres=None, bool want_dx_colsum=False, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, Tensor(c!)? dxs_out=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("embed_layernorm_fwd(Tensor idx, Tensor wte, Tensor wpe, Tensor w, Tensor? b, float eps) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("embed_scatter_add_(Tensor dx, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("embed_id_error(int device) -> int", &embed_id_error);
   m.def("batch_sum_(Tensor x, Tensor(a!) out) -> ()");
   m.def("add_layernorm_fwd(Tensor x, Tensor r, Tensor w, Tensor? b, float eps, Tensor? rbias=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor x, Tensor? b) -> Tensor");

@@ -20,12 +20,18 @@ namespace orion {
 __global__ __launch_bounds__(256) void embed_scatter_add_kernel(const bf16_t* __restrict__ dx,
                                                                 const int64_t* __restrict__ idx,
                                                                 float* __restrict__ out, long rows,
-                                                                int C) {
+                                                                int C, long V, int* err) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
+  const long id = idx[row];
+  ORION_DASSERT(id >= 0 && id < V);
+  if ((unsigned long)id >= (unsigned long)V) {  // never an atomic outside the table: flag it
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
   const bf16_t* d = dx + row * C;
-  float* o = out + idx[row] * C;
+  float* o = out + id * C;
   for (int c = lane; c < C; c += 64) atomicAdd(o + c, bf2f(d[c]));
 }
 
@@ -60,10 +66,10 @@ using namespace orion;
 extern "C++" {
 
 int orion_embed_scatter_add(const void* dx, const int64_t* idx, float* out, long rows, int C,
-                            hipStream_t st) {
+                            long V, int* err, hipStream_t st) {
   if (rows == 0) return 0;
   embed_scatter_add_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>((const bf16_t*)dx, idx, out,
-                                                                        rows, C);
+                                                                        rows, C, V, err);
   return (int)hipGetLastError();
 }
 

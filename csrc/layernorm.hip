@@ -36,13 +36,24 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
     int rows, int C, float eps, const bf16_t* __restrict__ res, bf16_t* __restrict__ sum_out,
-    const bf16_t* __restrict__ rbias, const int64_t* __restrict__ idx, int T) {
+    const bf16_t* __restrict__ rbias, const int64_t* __restrict__ idx, int T, long V, int* err) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   // idx: embedding gather -- x is the token table (row idx[row]) and res the position table
-  // (row row % T), so s = wte[idx] + wpe[t] is formed, returned and normalised in one pass
-  const bf16_t* xr = x + (size_t)(idx ? idx[row] : row) * C;
+  // (row row % T), so s = wte[idx] + wpe[t] is formed, returned and normalised in one pass.
+  // An id outside [0, V) never addresses memory: it reads table row 0 and raises the error
+  // flag (ops/embedding.py reports it).
+  long id = row;
+  if (idx) {
+    id = idx[row];
+    ORION_DASSERT(id >= 0 && id < V);
+    if ((unsigned long)id >= (unsigned long)V) {
+      if (lane == 0) atomicOr(err, 1);
+      id = 0;
+    }
+  }
+  const bf16_t* xr = x + (size_t)id * C;
   const size_t rrow = idx ? (size_t)(row % T) : (size_t)row;
   float v[ITERS][VEC];
   float s = 0.f;
@@ -358,7 +369,8 @@ int orion_ln_max_cols() { return 2048; }
 
 int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
                         float* rstd, int rows, int C, float eps, const void* res, void* sum_out,
-                        const void* rbias, hipStream_t st, const int64_t* idx, int T) {
+                        const void* rbias, hipStream_t st, const int64_t* idx, int T, long V,
+                        int* err) {
   int vec, it;
   if (!ln_pick(C, &vec, &it)) return -1;
   dim3 grid((rows + 3) / 4), block(256);
@@ -367,17 +379,17 @@ int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, fl
   auto R = (const bf16_t*)res; auto S = (bf16_t*)sum_out; auto RB = (const bf16_t*)rbias;
   if (vec == 8) {
     switch (it) {
-      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
-      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
-      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
-      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 1: ln_fwd_kernel<8, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
+      case 2: ln_fwd_kernel<8, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
+      case 3: ln_fwd_kernel<8, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
+      case 4: ln_fwd_kernel<8, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
     }
   } else {
     switch (it) {
-      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
-      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
-      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
-      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T); break;
+      case 1: ln_fwd_kernel<4, 1><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
+      case 2: ln_fwd_kernel<4, 2><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
+      case 3: ln_fwd_kernel<4, 3><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
+      case 4: ln_fwd_kernel<4, 4><<<grid, block, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps, R, S, RB, idx, T, V, err); break;
     }
   }
   return (int)hipGetLastError();

@@ -13,8 +13,15 @@ other add+LayerNorm), then
     producers before it reports the parameter to the data-parallel reducer
     (ops/grad_sink.py).  Deterministic mode and gradient-accumulation steps whose slice
     cannot be written directly use the sort-based dense embedding backward.
+
+Token ids are validated: the first call per device checks ``idx`` against the table on the
+host (one ``aminmax``; ``ORION_CHECK_IDS=1`` checks every call, at the price of a sync) and
+raises ``IndexError``, and both kernels clamp / skip any id outside ``[0, V)`` and raise a
+device flag instead of reading or atomically adding outside the table (``id_error``).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -22,6 +29,24 @@ from ._ext import C
 from .determinism import deterministic
 from .grad_sink import sink_of
 from .layernorm import _bf16, _claim, _grad, _notify, _unless, _view
+
+_CHECK_ALWAYS = os.environ.get("ORION_CHECK_IDS") == "1"
+_checked: set = set()
+
+
+def check_ids(idx, V):
+    """Raise IndexError if any token id is outside [0, V) (synchronises)."""
+    lo, hi = torch.aminmax(idx)
+    lo, hi = int(lo), int(hi)
+    if lo < 0 or hi >= V:
+        raise IndexError(f"token id out of range: ids span [{lo}, {hi}] for a table of {V} rows")
+
+
+def id_error(device=None) -> bool:
+    """True if an embedding kernel saw an out-of-range token id since the last call on this
+    device (the flag is cleared; synchronises the current stream)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    return bool(C().embed_id_error(dev.index if dev.index is not None else 0))
 
 
 def _dense_table_grad(dx2, idx, V):
@@ -80,14 +105,14 @@ class _EmbedLayerNorm(torch.autograd.Function):
                 if not acc:  # first producer of the step: the slice is not pre-zeroed
                     st.view.zero_()
                 C().embed_scatter_add_(dx2, idx, st.view.view(-1, Cc))
-                st.notify()
+                st.notify(last=True)
             elif st is not None:
                 g = _dense_table_grad(dx2, idx, wte.shape[0])
                 if st.take():
                     st.view.view(-1, Cc).add_(g)
                 else:
                     st.view.view(-1, Cc).copy_(g)
-                st.notify()
+                st.notify(last=True)
             else:
                 dwte = _dense_table_grad(dx2, idx, wte.shape[0]).to(wte.dtype)
         return (None, dwte, dwpe, _grad(dw, w.dtype),
@@ -95,4 +120,7 @@ class _EmbedLayerNorm(torch.autograd.Function):
 
 
 def embed_layer_norm_hip(idx, wte, wpe, weight, bias, eps=1e-5):
+    if _CHECK_ALWAYS or idx.device not in _checked:
+        check_ids(idx, wte.shape[0])
+        _checked.add(idx.device)
     return _EmbedLayerNorm.apply(idx.long(), wte, wpe, weight, bias, eps)

@@ -15,13 +15,18 @@ over micro-batches) -- and return ``None`` for the weight.  Because no
 data-parallel reducer's bucket counter) itself.
 
 Tied parameters (used by ``uses`` > 1 modules, e.g. GPT-2's ``wte`` = LM head) get a sink
-too: the first write of a step overwrites, every later one accumulates (``take``).  Their
-``notify`` reports nothing: how many producers of a micro-step write through the sink
-depends on the graph (the GPT-2 input op does; a dropout path's plain embedding goes
-through ``AccumulateGrad`` and the arena's fold hook), so the parameter is reported by its
-post-accumulate-grad hook, which autograd runs once per backward after the LAST use's
-contribution -- a data-parallel bucket is never launched between the LM head's and the
-embedding's writes.
+too: the first write of a step overwrites, every later one accumulates (``take``).  A
+producer that is not the parameter's last use in the backward (the LM head) calls
+``notify()``, which only counts.  The last use (GPT-2's fused embedding, the final kernel of
+the backward) calls ``notify(last=True)``: the parameter is reported once every ``expect``
+producer of this micro-step has written through the sink.  When some use of the micro-step
+did not (a dropout path's plain embedding goes through ``AccumulateGrad`` and the arena's
+fold hook, and never calls ``notify(last=True)``), nothing is reported here and the
+post-accumulate-grad hook reports the parameter after that last contribution instead.
+Either way a data-parallel bucket is never launched between the LM head's and the
+embedding's writes -- and, since ``AccumulateGrad`` runs no hook for an undefined
+gradient, the all-sink case is reported during the backward rather than only at
+``finish()``.
 ``ORION_DIRECT_GRADS=0`` disables the mechanism.
 """
 from __future__ import annotations
@@ -35,13 +40,15 @@ ENABLED = os.environ.get("ORION_DIRECT_GRADS", "1") != "0"
 
 
 class GradSink:
-    __slots__ = ("view", "fresh", "expect", "notes", "_param", "_listeners", "__weakref__")
+    __slots__ = ("view", "fresh", "expect", "notes", "_micro", "_param", "_listeners",
+                 "__weakref__")
 
     def __init__(self, param: torch.Tensor, view: torch.Tensor, listeners: list, expect: int = 1):
         self.view = view            # the parameter's slice of the gradient arena, param-shaped
         self.fresh = True           # no write yet this step -> the next write may overwrite
         self.expect = expect        # producers per micro-step (uses of a tied parameter)
         self.notes = 0              # notify() calls since the step began
+        self._micro = 0             # notify() calls since the last use's notify(last=True)
         self._param = weakref.ref(param)
         self._listeners = listeners  # shared with the owning arena
 
@@ -49,6 +56,7 @@ class GradSink:
         """Start of an optimizer step (the arena's zero_grad)."""
         self.fresh = True
         self.notes = 0
+        self._micro = 0
 
     def take(self) -> bool:
         """Claim the slice for one write; returns True if the write must accumulate."""
@@ -56,10 +64,18 @@ class GradSink:
         self.fresh = False
         return acc
 
-    def notify(self):
+    def notify(self, last: bool = False):
+        """One producer wrote its gradient through the sink.  ``last``: the producer is the
+        parameter's last use in the backward (only meaningful for tied parameters)."""
         self.notes += 1
+        self._micro += 1
         if self.expect > 1:
-            return  # tied: reported by the parameter's post-accumulate hook (module docstring)
+            if not last:
+                return
+            complete = self._micro >= self.expect
+            self._micro = 0
+            if not complete:  # some use went through AccumulateGrad: its hook reports
+                return
         p = self._param()
         if p is not None:
             for cb in self._listeners:

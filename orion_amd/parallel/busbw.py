@@ -48,6 +48,32 @@ def allreduce_busbw(buf, iters: int = 10, warmup: int = 2, group=None) -> float:
     return round(nbytes / float(t) * 2 * (world - 1) / world / 1e9, 2)
 
 
+def rccl_summary(path: str) -> dict | None:
+    """Topology facts from one rank's RCCL INFO log (``launch.rccl_debug_env``): channel
+    count, the first rings, the collective/p2p channel line and the RCCL version."""
+    import re
+    try:
+        with open(path, errors="replace") as f:
+            text = f.read()
+    except OSError:
+        return None
+    chans = re.findall(r"Channel (\d+)/(\d+) :\s*([\d ]+)", text)
+    out = {"log": path}
+    if chans:
+        out["channels"] = max(int(t) for _, t, _ in chans)
+        out["rings"] = [" ".join(r.split()) for _, _, r in chans[:2]]
+    m = re.search(r"(\d+) coll channels,.*", text)
+    if m:
+        out["coll_channels"] = m.group(0).strip()
+    m = re.search(r"RCCL version[^\n]*", text) or re.search(r"NCCL version[^\n]*", text)
+    if m:
+        out["version"] = m.group(0).strip()
+    m = re.findall(r"Trees? \[0\][^\n]*", text)
+    if m:
+        out["tree0"] = m[0].strip()
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=8)
@@ -65,10 +91,7 @@ def main(argv=None):
     dev = launch.device_for(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)), args.backend)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    if args.backend == "nccl":
-        dist.init_process_group("nccl", device_id=dev)
-    else:
-        dist.init_process_group(args.backend)
+    launch.init_process_group(args.backend, dev if args.backend == "nccl" else None)
     for dt in args.dtypes.split(","):
         dtype = getattr(torch, dt)
         for mb in (float(x) for x in args.sizes_mb.split(",")):

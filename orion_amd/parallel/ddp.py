@@ -24,12 +24,26 @@ Design (MI355X-first, not a translation of any NCCL call pattern):
   gradient is complete only after the embedding backward, the last kernel of the
   pass, and would otherwise hold back every layer sharing its bucket;
 * gradient accumulation: reduction is only armed on the last micro-step
-  (``set_sync``), the same contract as DDP's ``no_sync``.
+  (``set_sync``), the same contract as DDP's ``no_sync``;
+* observability (``timing=True``): per bucket, the moment its gradients were ready on the
+  compute stream and the moment its collective completed (HIP events: the completion
+  event is recorded on a side stream made to wait for the collective), plus the end of the
+  backward, so ``timing_report()`` gives each bucket's launch->complete time and the
+  exposed communication tail (last completion minus backward end) of the last step;
+* fail-fast: a watchdog thread (``ORION_DDP_WATCHDOG_S``, default 180 s, 0 = off) checks
+  the launched collectives; one that has not completed in time makes the rank print which
+  bucket of which step it was stuck on and exit 124, instead of the job hanging inside RCCL
+  until the driver's own limit.
 
 Works with any ``torch.distributed`` backend: ``nccl`` (= RCCL on ROCm) on
 GPUs, ``gloo`` on CPU for the multi-process tests.
 """
 from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -46,9 +60,47 @@ def default_bucket_mb(n_params: int) -> float:
     return 256.0 if n_params >= 1_000_000_000 else 64.0
 
 
+class _Watchdog(threading.Thread):
+    """Polls the reducer's launched collectives; a bucket pending longer than ``limit``
+    seconds ends the process with a message naming it (exit 124)."""
+
+    def __init__(self, limit: float, rank: int):
+        super().__init__(name="orion-ddp-watchdog", daemon=True)
+        self.limit = limit
+        self.rank = rank
+        self.pending: list = []          # (step, bucket, t_launch, work, numel)
+        self.lock = threading.Lock()
+        self.stop = threading.Event()
+
+    def add(self, step, bucket, work, numel):
+        with self.lock:
+            self.pending.append((step, bucket, time.monotonic(), work, numel))
+
+    def run(self):
+        while not self.stop.wait(1.0):
+            with self.lock:
+                live = []
+                for rec in self.pending:
+                    try:
+                        done = rec[3].is_completed()
+                    except Exception:  # noqa: BLE001 -- a failed collective is reported below
+                        done = False
+                    if not done:
+                        live.append(rec)
+                self.pending = live
+                late = [r for r in live if time.monotonic() - r[2] > self.limit]
+            if late:
+                step, bi, t0, _, numel = late[0]
+                print(f"[orion_amd.ddp] rank {self.rank}: all-reduce of bucket {bi} "
+                      f"({numel} elements) of step {step} not complete after "
+                      f"{time.monotonic() - t0:.0f} s ({len(live)} collective(s) pending); "
+                      f"aborting", file=sys.stderr, flush=True)
+                os._exit(124)
+
+
 class GradBucketReducer:
     def __init__(self, arena: FlatArena, bucket_mb: float | None = None, group=None,
-                 average: bool = True):
+                 average: bool = True, timing: bool = False, watchdog_s: float | None = None):
         if bucket_mb is None or bucket_mb <= 0:
             bucket_mb = default_bucket_mb(arena.numel)
         self.arena = arena
@@ -98,6 +150,52 @@ class GradBucketReducer:
         arena.grad_listeners.append(self._on_grad)
         avg = getattr(dist.ReduceOp, "AVG", None)
         self._use_avg_op = average and avg is not None and dist.get_backend(group) == "nccl"
+        self.step = 0
+        # per-bucket timing of the last armed step (events on the GPU, host clock on the CPU)
+        self.timing = timing
+        self._cuda = arena.grads.is_cuda
+        self._tstream = None
+        self._t0 = self._bwd_end = None
+        self._t_ready = [None] * len(self.buckets)
+        self._t_done = [None] * len(self.buckets)
+        if watchdog_s is None:
+            watchdog_s = float(os.environ.get("ORION_DDP_WATCHDOG_S", "180"))
+        self._watchdog = None
+        if watchdog_s > 0 and self.world > 1:
+            self._watchdog = _Watchdog(watchdog_s, dist.get_rank(group))
+            self._watchdog.start()
+
+    # ------------------------------------------------------------------ timing
+    def _mark(self):
+        if self._cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
+
+    def timing_report(self):
+        """Bucket timeline of the last armed step in ms from the step's first ready bucket:
+        ``buckets`` = [(index, MB, ready, done)], ``bwd_end``, ``exposed_tail_ms`` = last
+        completion - backward end (> 0: communication the backward did not hide).  Syncs."""
+        if not self.timing or self._bwd_end is None or any(t is None for t in self._t_done):
+            return None
+        if self._cuda:
+            torch.cuda.synchronize()
+            ref = self._t_ready[0]
+            rel = lambda ev: ref.elapsed_time(ev)  # noqa: E731
+        else:
+            ref = self._t_ready[0]
+            rel = lambda t: (t - ref) * 1e3  # noqa: E731
+        esize = self.arena.grads.element_size()
+        rows = []
+        for bi, (b0, b1, _) in enumerate(self.buckets):
+            rows.append((bi, round((b1 - b0) * esize / 2**20, 2), round(rel(self._t_ready[bi]), 3),
+                         round(rel(self._t_done[bi]), 3)))
+        bwd = rel(self._bwd_end)
+        last = max(r[3] for r in rows)
+        return {"buckets": rows, "bwd_end_ms": round(bwd, 3),
+                "exposed_tail_ms": round(max(0.0, last - bwd), 3),
+                "comm_ms": round(sum(r[3] - r[2] for r in rows), 3)}
 
     def _aligned_end(self, slot):
         from ..train.flat import ALIGN
@@ -143,16 +241,34 @@ class GradBucketReducer:
         b0, b1, _ = self.buckets[bi]
         view = self.arena.grads[b0:b1]
         op = dist.ReduceOp.AVG if self._use_avg_op else dist.ReduceOp.SUM
-        self._handles[bi] = dist.all_reduce(view, op=op, group=self.group, async_op=True)
+        if self.timing:
+            self._t_ready[bi] = self._mark()
+        h = dist.all_reduce(view, op=op, group=self.group, async_op=True)
+        self._handles[bi] = h
+        if self.timing and self._cuda:
+            # completion: a side stream waits for the collective, then records
+            if self._tstream is None:
+                self._tstream = torch.cuda.Stream()
+            with torch.cuda.stream(self._tstream):
+                h.wait()
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(self._tstream)
+            self._t_done[bi] = ev
+        if self._watchdog is not None:
+            self._watchdog.add(self.step, bi, h, b1 - b0)
 
     def finish(self):
         """Launch stragglers (unused params), wait for every bucket, reset counters."""
         if not self._sync:
             return
+        if self.timing:
+            self._bwd_end = self._mark()
         self._ready = [True] * len(self.buckets)
         self._flush()
         for bi, h in enumerate(self._handles):
             h.wait()
+            if self.timing and not self._cuda:
+                self._t_done[bi] = time.perf_counter()
             if self.average and not self._use_avg_op:
                 b0, b1, _ = self.buckets[bi]
                 self.arena.grads[b0:b1].div_(self.world)
@@ -160,8 +276,12 @@ class GradBucketReducer:
         self._arrived = [set() for _ in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._cursor = 0
+        self.step += 1
 
     def remove(self):
+        if self._watchdog is not None:
+            self._watchdog.stop.set()
+            self._watchdog = None
         for h in self._hooks:
             h.remove()
         self._hooks = []

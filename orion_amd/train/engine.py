@@ -69,7 +69,7 @@ class Trainer:
 
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float | None = None, arena_dtype=None,
-                 graph: bool = False, grad_dtype=None):
+                 graph: bool = False, grad_dtype=None, ddp_timing: bool = False):
         self.model = model
         self.cfg = optim or OptimConfig()
         dev = next(model.parameters()).device
@@ -89,7 +89,7 @@ class Trainer:
         self.reducer = None
         if ddp:
             from ..parallel.ddp import GradBucketReducer
-            self.reducer = GradBucketReducer(self.arena, bucket_mb=bucket_mb)
+            self.reducer = GradBucketReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing)
             # R1: every rank starts from rank 0's exact fp32 weights
             dist.broadcast(self.opt.master, 0)
             with torch.no_grad():

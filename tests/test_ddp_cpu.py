@@ -173,9 +173,69 @@ def test_bench_spawns_its_own_ranks_on_cpu():
     assert rec["steps"] == 2 and rec["warmup"] == 1
     assert abs(rec["per_gpu"] * 2 - rec["value"]) / rec["value"] < 1e-3
     assert rec["allreduce_busbw_gbps"] is not None
+    # bucket timeline of the last step: every bucket ready before it completed
+    ddp = rec["ddp_buckets"]
+    assert ddp is not None and ddp["exposed_tail_ms"] >= 0
+    assert all(done >= ready for _, _, ready, done in ddp["buckets"])
 
 
 def test_default_bucket_size_by_model_size():
     from orion_amd.parallel.ddp import default_bucket_mb
     assert default_bucket_mb(124_000_000) == 64.0
     assert default_bucket_mb(6_740_000_000) == 256.0
+
+
+def _divergent_worker(rank, world, port, out):
+    """Ranks see their gradients arrive in DIFFERENT orders and each rank has a different
+    parameter that never gets a gradient (launched only by finish)."""
+    import random
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from orion_amd.parallel.launch import init_process_group
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world))
+    init_process_group("gloo")
+    from orion_amd.parallel.ddp import GradBucketReducer
+    from orion_amd.train.flat import FlatArena
+    torch.manual_seed(0)
+    arena = FlatArena(build_gpt2("gpt2-tiny", block_size=32), dtype=torch.float32)
+    red = GradBucketReducer(arena, bucket_mb=0.05, timing=True, watchdog_s=60.0)
+    red.launch_log = []
+    logs = []
+    for step in range(2):
+        arena.grads.fill_(float(rank + 1))
+        red.set_sync(True)
+        slots = [s for _, _, sl in red.buckets for s in sl]
+        order = list(range(len(slots)))
+        random.Random(1000 * rank + step).shuffle(order)
+        unused = slots[(7 * rank + step) % len(slots)].param
+        for i in order:
+            if slots[i].param is not unused:
+                red._on_grad(slots[i].param)
+        red.finish()
+        logs.append(list(red.launch_log))
+        red.launch_log = []
+    rep = red.timing_report()
+    out.put((rank, logs, arena.grads.clone().numpy(), len(red.buckets), rep is not None))
+    red.remove()
+    dist.destroy_process_group()
+
+
+def test_divergent_arrival_orders_and_unused_params_four_ranks():
+    """SURVEY §7.6 tests/dist: 4 gloo ranks whose gradient arrival orders differ and each
+    with a rank-dependent unused parameter: no hang, every rank issues the collectives in the
+    same (bucket) order, and the reduced gradient is the average over ranks."""
+    world = 4
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_divergent_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    nb = res[0][3]
+    assert nb >= 4
+    for rank, logs, grads, _, timed in res:
+        assert logs == [list(range(nb))] * 2, (rank, logs)
+        assert timed
+        assert torch.allclose(torch.from_numpy(grads), torch.full_like(torch.from_numpy(grads), 2.5))
