@@ -40,7 +40,12 @@ def report_results(data):
     if isinstance(data, list):
         data = [dict(d, value=_plain(d.get("value"))) for d in data]
     if IS_METAOPT_ON:
-        if int(os.environ.get("RANK", "0")) == 0:
+        rank = int(os.environ.get("RANK", "0"))
+        audit = os.environ.get("ORION_REPORT_AUDIT")  # tests: one line per call, any rank
+        if audit:
+            with open(audit, "a") as f:
+                f.write(f"{rank} {os.getpid()}\n")
+        if rank == 0:
             with open(RESULTS_FILENAME, "w") as f:
                 json.dump(data, f)
     else:

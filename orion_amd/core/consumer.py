@@ -18,6 +18,10 @@ MI355X-node additions:
   the trial no longer ``reserved`` (a reaper re-queued it because this worker
   looked dead), the child is stopped and the trial is abandoned without writing
   anything, so no trial is ever completed twice;
+* the GPU lease follows the process that uses the GPUs: the child inherits the lease's
+  lock files (``pass_fds``), so a SIGKILLed worker's devices stay locked while its
+  orphaned trial lives, and the child gets ``PR_SET_PDEATHSIG`` (SIGTERM) so such an
+  orphan is told to stop at once instead of training on for a result nobody records;
 * ``trial_timeout``: the child is killed and the trial marked ``broken``;
 * SIGINT/SIGTERM of the worker: the child is terminated and the trial is
   returned to the pool as ``interrupted`` (the reference had the status but
@@ -39,6 +43,19 @@ import time
 from .trial import Trial
 
 log = logging.getLogger(__name__)
+
+
+def _term_with_parent(parent_pid):
+    """preexec_fn of a trial process: SIGTERM when the worker dies (any way it dies)."""
+    def arm():
+        try:
+            import ctypes
+            ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+        if os.getppid() != parent_pid:
+            os._exit(1)
+    return arm
 
 
 class TrialInterrupted(Exception):
@@ -171,7 +188,7 @@ class Consumer:
                     "--local-addr", "127.0.0.1", f"--nproc-per-node={self.gpus_per_trial}", script]
         return base + list(cmd_args)
 
-    def launch_process(self, results_filename, cmd_args, extra_env=None):
+    def launch_process(self, results_filename, cmd_args, extra_env=None, pass_fds=()):
         env = dict(os.environ)
         env["METAOPT_RESULTS_PATH"] = str(results_filename)
         env["ORION_RESULTS_PATH"] = str(results_filename)
@@ -180,16 +197,19 @@ class Consumer:
         cmd = self.command(cmd_args)
         log.debug("launching %s", cmd)
         try:
-            return subprocess.Popen(cmd, env=env, start_new_session=True)
+            return subprocess.Popen(cmd, env=env, start_new_session=True, pass_fds=tuple(pass_fds),
+                                    preexec_fn=_term_with_parent(os.getpid()))
         except OSError as exc:
             log.error("Failed to execute script to evaluate trial: %s", exc)
             return None
 
     def _run(self, results_filename, cmd_args, trial, lease):
         extra = {"ORION_TRIAL_ID": str(trial.id)}
+        fds = ()
         if lease is not None:
             extra.update(lease.env())
-        proc = self.launch_process(results_filename, cmd_args, extra)
+            fds = lease.fds
+        proc = self.launch_process(results_filename, cmd_args, extra, pass_fds=fds)
         if proc is None:
             return -1
         t0 = time.monotonic()

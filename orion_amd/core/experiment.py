@@ -172,18 +172,26 @@ class Experiment:
         if not only_if_reserved:
             self._db.write("trials", doc, query={"_id": trial.id})
             return True
-        q = {"_id": trial.id, "status": "reserved"}
-        if getattr(trial, "worker", None) is not None:
-            q["worker"] = trial.worker
+        q = self._owned(trial)
         doc.pop("_id", None)
         return self._db.read_and_write("trials", q, doc) is not None
 
+    @staticmethod
+    def _owned(trial, status="reserved"):
+        """CAS query for a trial this worker holds: its id, the expected status and -- when
+        the trial carries the reserving worker's id -- that worker.  A trial that a reaper
+        re-queued and another worker reserved is then out of reach of the first worker's
+        heartbeats, leases and status writes."""
+        q = {"_id": trial.id, "status": status}
+        if getattr(trial, "worker", None) is not None:
+            q["worker"] = trial.worker
+        return q
+
     def set_trial_status(self, trial, status, only_if=None):
-        """Move ``trial`` to ``status``; with ``only_if`` it is a CAS on the current status."""
+        """Move ``trial`` to ``status``; with ``only_if`` it is a CAS on the current status
+        (and on the reserving worker, see :meth:`_owned`)."""
+        q = {"_id": trial.id} if only_if is None else self._owned(trial, only_if)
         trial.status = status
-        q = {"_id": trial.id}
-        if only_if is not None:
-            q["status"] = only_if
         upd = {"status": status}
         if status in ("broken", "completed"):
             upd["end_time"] = trial.end_time = utcnow()
@@ -194,7 +202,7 @@ class Experiment:
         ``start_time`` from the reservation to now (a reserved trial may wait for a GPU
         lease first).  False if the trial is no longer ours."""
         now = utcnow()
-        ok = self._db.read_and_write("trials", {"_id": trial.id, "status": "reserved"},
+        ok = self._db.read_and_write("trials", self._owned(trial),
                                      {"gpus": list(gpu_ids), "start_time": now,
                                       "heartbeat": now}) is not None
         if ok:
@@ -202,7 +210,7 @@ class Experiment:
         return ok
 
     def update_heartbeat(self, trial):
-        return self._db.read_and_write("trials", {"_id": trial.id, "status": "reserved"},
+        return self._db.read_and_write("trials", self._owned(trial),
                                        {"heartbeat": utcnow()}) is not None
 
     def fix_lost_trials(self, timeout_s):

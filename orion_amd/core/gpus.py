@@ -6,6 +6,13 @@ worker *processes* never place two trials on one GPU.  The lease is exported
 to the trial as ``HIP_VISIBLE_DEVICES`` (and ``CUDA_VISIBLE_DEVICES``/
 ``ROCR_VISIBLE_DEVICES`` left untouched).  Locks die with the process, so a
 crashed worker cannot leak a GPU.
+
+The lock belongs to the open lock file, which the trial process inherits
+(``Consumer`` passes ``lease.fds`` to the child): a GPU stays locked exactly as long
+as some process that may be using it lives.  A worker that is SIGKILLed mid-trial
+therefore does not free its GPU while its trial (or its trial's torchrun launcher)
+still runs -- the reaper may re-queue the trial, but no other worker can place it,
+or anything else, on that device until the orphan has exited.
 """
 from __future__ import annotations
 
@@ -33,6 +40,11 @@ class GPULease:
     def __init__(self, ids, fds):
         self.ids = ids
         self._fds = fds
+
+    @property
+    def fds(self):
+        """The open lock files (to hand to the trial process: ``Popen(pass_fds=...)``)."""
+        return tuple(self._fds)
 
     def env(self):
         return {"HIP_VISIBLE_DEVICES": ",".join(self.ids)} if self.ids else {}

@@ -1,6 +1,12 @@
 """Producer (component C7, ``src/orion/core/worker/producer.py``): feeds newly
-completed trials to the algorithm (``observe``) and registers ``pool_size`` new
-suggestions as ``new`` trials."""
+completed trials to the algorithm (``observe``) and registers new suggestions as
+``new`` trials.
+
+Budget (fixed rather than copied): the reference always
+registered ``pool_size`` points (``producer.py:35-45``), so W workers could overshoot
+``max_trials`` by ~W x pool_size trials -- each one a GPU training run here.  ``produce``
+asks for at most ``max_trials`` minus the trials that are still going to count
+(every status but ``broken``), and nothing once that is reached."""
 from __future__ import annotations
 
 import logging
@@ -20,8 +26,22 @@ class Producer:
         self.algorithm = experiment.algorithms
         self.num_new_trials = experiment.pool_size
 
+    def budget(self):
+        """How many more trials may be registered: ``pool_size``, capped by what is left of
+        ``max_trials`` after the registered non-broken trials."""
+        max_trials = getattr(self.experiment, "max_trials", float("inf"))
+        n = self.num_new_trials
+        if max_trials is not None and max_trials != float("inf"):
+            live = self.experiment.count_trials(
+                ("new", "reserved", "suspended", "interrupted", "completed"))
+            n = min(n, int(max_trials) - live)
+        return max(0, n)
+
     def produce(self):
-        points = self.algorithm.suggest(self.num_new_trials)
+        n = self.budget()
+        if n <= 0:
+            return 0
+        points = self.algorithm.suggest(n)
         trials = [format_trials.tuple_to_trial(p, self.space) for p in points]
         log.debug("registering %d new trial(s)", len(trials))
         self.experiment.register_trials(trials)

@@ -6,9 +6,12 @@ experiment is done, else produce ``pool_size`` new trials.  Workers on one or
 many nodes coordinate only through the store's compare-and-swap.
 
 Additions: exponential idle back-off instead of a hot spin on the database,
-a stale-reservation reaper (heartbeat timeout), a broken-trial budget, and
+a stale-reservation reaper (heartbeat timeout), a broken-trial budget,
 ``workon_pool`` to run several workers (each its own process, each leasing its
-own GPUs) on one MI355X node.
+own GPUs) on one MI355X node, and a trial budget that holds: a worker does not
+reserve another trial while completed + reserved trials already reach
+``max_trials`` (it waits for the running ones to complete or break), and the
+producer never registers more than the budget leaves (``producer.py``).
 """
 from __future__ import annotations
 
@@ -33,17 +36,22 @@ def workon(experiment, gpus_per_trial=0, heartbeat=30.0, trial_timeout=None, max
                         heartbeat=heartbeat, trial_timeout=trial_timeout, worker_id=worker_id)
     broken = 0
     sleep = idle_sleep[0]
-    stale_after = max(3 * heartbeat, 30.0)
+    # a reservation whose heartbeat is older than this is re-queued (floor: 30 s, or
+    # ORION_STALE_AFTER_MIN_S for tests that exercise the reaper)
+    stale_after = max(3 * heartbeat, float(os.environ.get("ORION_STALE_AFTER_MIN_S", "30")))
     log.debug("#####  Init Experiment  #####")
+    budgeted = experiment.max_trials not in (None, float("inf"))
     while True:
-        trial = experiment.reserve_trial(score_handle=producer.algorithm.score, worker=worker_id)
+        trial = None
+        if not budgeted or experiment.count_trials(("completed", "reserved")) < experiment.max_trials:
+            trial = experiment.reserve_trial(score_handle=producer.algorithm.score, worker=worker_id)
         if trial is None:
             producer.update()
             if experiment.finish_if_done():
                 break
             experiment.fix_lost_trials(stale_after)
-            if experiment.count_trials(("new", "suspended", "interrupted")) == 0:
-                producer.produce()
+            if (experiment.count_trials(("new", "suspended", "interrupted")) == 0
+                    and producer.produce() > 0):
                 sleep = idle_sleep[0]
             else:
                 time.sleep(sleep)

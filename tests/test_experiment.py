@@ -210,6 +210,35 @@ def test_completion_is_a_cas_on_reserved(storage):
     assert doc["status"] in ("reserved", "interrupted") and doc.get("results", []) == []
 
 
+def test_lost_trial_is_out_of_reach_of_its_first_worker(storage):
+    """The reaper re-queues w0's trial and w1 reserves it: w0's heartbeat, lease record and
+    'broken' / 'interrupted' writes must all fail and leave w1's reservation untouched
+    (they used to check only the status)."""
+    exp = _ready(storage)
+    exp.pool_size = 1
+    Producer(exp).produce()
+    t0 = exp.reserve_trial(worker="w0")
+    assert t0 is not None and t0.worker == "w0"
+    storage.write("trials", {"heartbeat": utcnow() - datetime.timedelta(hours=1)}, {"_id": t0.id})
+    assert exp.fix_lost_trials(60) == 1
+    t1 = exp.reserve_trial(worker="w1")
+    assert t1 is not None and t1.id == t0.id and t1.worker == "w1"
+    before = storage.read("trials", {"_id": t0.id})[0]
+    assert not exp.update_heartbeat(t0)
+    assert not exp.record_lease(t0, [3])
+    assert not exp.set_trial_status(t0, "broken", only_if="reserved")
+    assert not exp.set_trial_status(t0, "interrupted", only_if="reserved")
+    t0.results = [Trial.Result(name="o", type="objective", value=1.0)]
+    assert not exp.push_completed_trial(t0, only_if_reserved=True)
+    after = storage.read("trials", {"_id": t0.id})[0]
+    assert after["status"] == "reserved" and after["worker"] == "w1"
+    assert after.get("heartbeat") == before.get("heartbeat") and after.get("gpus") == before.get("gpus")
+    # the rightful owner's writes still succeed
+    assert exp.update_heartbeat(t1) and exp.record_lease(t1, [0])
+    t1.results = [Trial.Result(name="o", type="objective", value=2.0)]
+    assert exp.push_completed_trial(t1, only_if_reserved=True)
+
+
 def test_plan_configuration_is_pure(storage):
     from orion_amd.core.experiment import plan_configuration
     exp = Experiment("p", storage, user="u")

@@ -639,9 +639,10 @@ def test_embed_layer_norm_matches_reference():
 
 def test_tied_embedding_sink_reports_after_both_producers():
     """GPT-2's tied wte / LM head: the LM head's weight gradient and the embedding's
-    scatter-add both land in the fp32 arena slice; the sink itself reports nothing (its
-    listeners never see wte), the parameter's post-accumulate hook fires once per micro-step
-    after both writes, and the slice equals the AccumulateGrad path."""
+    scatter-add both land in the fp32 arena slice; the sink reports wte to its listeners
+    (the data-parallel reducer) once per micro-step, from the embedding backward -- the last
+    use -- after both writes, the parameter's post-accumulate hook fires once per micro-step
+    too, and the slice equals the AccumulateGrad path."""
     from orion_amd.models.gpt2 import build_gpt2
     from orion_amd.train.flat import FlatArena
     torch.manual_seed(0)
@@ -651,9 +652,14 @@ def test_tied_embedding_sink_reports_after_both_producers():
     a2.detach_sinks()
     wte = m1.transformer.wte.weight
     assert wte._orion_sink.expect == 2
-    seen, hooked = [], []
-    a1.grad_listeners.append(lambda p: seen.append(p is wte))
+    seen, hooked, at_report = [], [], []
     s = next(s for s in a1.slots if s.param is wte)
+
+    def listener(p):
+        seen.append(p is wte)
+        if p is wte:
+            at_report.append(float(a1.grads[s.offset:s.offset + s.numel].float().norm()))
+    a1.grad_listeners.append(listener)
 
     def at_hook(p):  # the slice must already hold both contributions of this micro-step
         hooked.append(float(a1.grads[s.offset:s.offset + s.numel].float().norm()))
@@ -665,8 +671,50 @@ def test_tied_embedding_sink_reports_after_both_producers():
             _, loss = model(x, x)
             (loss / 2).backward()
         arena.finish_grads()
-    assert seen.count(True) == 0
+    assert seen.count(True) == 2
     assert len(hooked) == 2 and hooked[1] > hooked[0] > 0
+    # reported with both contributions of the micro-step in the slice (= what the hook sees)
+    assert at_report == pytest.approx(hooked, rel=1e-6)
     g1, g2 = (a.grads[s.offset:s.offset + s.numel] for a in (a1, a2))
     assert rel_err(g1, g2) < 1e-2
     assert rel_err(a1.grads, a2.grads) < 1e-2
+
+
+def test_embedding_rejects_out_of_range_ids():
+    """A token id outside the table raises on the host check, and the kernels themselves
+    never touch memory outside the table: an out-of-range id reads row 0 in the forward,
+    is skipped by the backward scatter, and raises the device error flag."""
+    from orion_amd import ops
+    from orion_amd.ops import embedding as emb
+    from orion_amd.ops._ext import C
+    torch.manual_seed(0)
+    V, Tm, Cc, B, T = 100, 64, 128, 2, 32
+    wte = (torch.randn(V, Cc, device=DEV) * 0.5).bfloat16()
+    wpe = (torch.randn(Tm, Cc, device=DEV) * 0.5).bfloat16()
+    w = torch.ones(Cc, device=DEV).bfloat16()
+    b = torch.zeros(Cc, device=DEV).bfloat16()
+    bad = torch.randint(0, V, (B, T), device=DEV)
+    bad[1, 5] = V + 7
+    with pytest.raises(IndexError):
+        emb.check_ids(bad, V)
+    emb._checked.discard(bad.device)
+    with pytest.raises(IndexError):
+        ops.embed_layer_norm(bad, wte, wpe, w, b)
+    bad[0, 3] = -1
+    assert not emb.id_error(DEV)
+    s_, y, _, _ = C().embed_layernorm_fwd(bad, wte, wpe, w, b, 1e-5)
+    torch.cuda.synchronize()
+    assert emb.id_error(DEV)
+    assert not emb.id_error(DEV)  # read clears it
+    assert torch.equal(s_[1, 5], (wte[0].float() + wpe[5].float()).bfloat16())
+    table = torch.zeros(V, Cc, device=DEV)
+    guard = torch.zeros(4 * V, Cc, device=DEV)  # memory after the table stays untouched
+    dx = torch.ones(B * T, Cc, device=DEV).bfloat16()
+    C().embed_scatter_add_(dx, bad, table)
+    torch.cuda.synchronize()
+    assert emb.id_error(DEV)
+    good = bad.clone().reshape(-1)
+    ok = (good >= 0) & (good < V)
+    want = torch.zeros(V, Cc, device=DEV).index_add_(0, good[ok], dx.float()[ok])
+    assert torch.equal(table, want)
+    assert float(guard.abs().max()) == 0.0

@@ -104,7 +104,8 @@ def main(argv=None):
             from orion_amd.parallel.launch import init_process_group
             init_process_group(cfg["backend"], torch.device("cuda", local_rank))
         else:
-            dist.init_process_group("gloo")
+            from orion_amd.parallel.launch import init_process_group
+            init_process_group("gloo")
     master = rank == 0
     device = torch.device(cfg["device"] if not cfg["device"].startswith("cuda") else f"cuda:{local_rank}")
     if device.type == "cuda":
