@@ -370,10 +370,11 @@ using namespace orion;
 // schedule), 0 = BK 64 x 2 stages, 1 = ping-pong, 2 = BK 32 x 4-stage ring,
 // 3 = BK 32 x 5-stage ring (160 KB: three stages in flight), 4/5/6 = 4 waves of 128 x 128
 // with BK 64 x 2 / BK 32 x 4 / BK 32 x 5 (docs/PERFORMANCE.md, "In-tree GEMM study").
+// 9 = the 16x16x32-MFMA phased kernel (csrc/gemm16.hip).
 static int gemm_cfg() {  // read per call: microbenchmarks switch variants in one process
   const char* e = getenv("ORION_GEMM_CFG");
   const int c = e ? atoi(e) : 7;
-  return c < 0 || c > 8 ? 7 : c;
+  return c < 0 || c > 9 ? 7 : c;
 }
 
 template <bool WKM, int EPI, int BK, int NS, int WM = 4>
@@ -451,7 +452,15 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   const int cfg = gemm_cfg();
   if (cfg == 8) a.flags |= 16;  // phased kernel, SCHED 0 (8-MFMA quadrant phases)
   int rc;
-  if ((cfg == 7 || cfg == 8) && gemm_phased_ok(a, wkm)) {
+  if (cfg == 9 && gemm_phased_ok(a, wkm) &&
+      (epi != EPI_GELU_BWD || (ldp % 8 == 0 && !(reinterpret_cast<uintptr_t>(pre) & 15)))) {
+    const int rows = (M + 63) / 64;
+    if (db) a.colsum = part;
+    rc = gemm16(a, wkm, epi, st);
+    if (rc == 0 && db) rc = orion_colsum_partials2(part, part + (long)rows * N, db, rows, N, db_f32, st);
+    return rc;
+  }
+  if ((cfg == 7 || cfg == 8 || cfg == 9) && gemm_phased_ok(a, wkm)) {
     const int rows = (M + 63) / 64;
     if (db) a.colsum = part;
     rc = gemm_phased(a, wkm, epi, st);

@@ -1,0 +1,479 @@
+// Phase-interleaved linear-layer GEMM on v_mfma_f32_16x16x32_bf16 (gfx950): forward (NT),
+// input gradient (NN) and weight gradient (k-major x k-major, split-K), fused epilogues.
+//
+// Same tile, wave roles and barrier schedule as csrc/gemm_phased.hip (SCHED 1), with the
+// 16x16x32 MFMA instead of 32x32x16.  On random operands the chip holds a higher clock on the
+// 16x16x32 shape at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7:
+// ~1.12-1.15x FLOP/s in LDS-fed loops), which is the gap between the 32x32 phased kernel
+// (~1.15 PF/s at 4096^3) and the 16x16 8-phase template of the CDNA guide (~1.32 PF/s).
+//
+// Tile 256 (n) x 256 (m) per 512-thread workgroup, one workgroup per work item, K in 64-deep
+// k-tiles.  Swapped orientation: the W tile is the A operand (rows n), the X tile the B
+// operand (columns m), the accumulators hold C^T.  8 waves = 2 groups (grp = n half of 128) x
+// 4 (wm = 64 m rows); a wave owns 128 n x 64 m = 8 x 4 accumulators of 16 x 16.
+//
+// Schedule (per k-tile, two phases H = 0, 1; group 1 runs one barrier slot behind group 0, so
+// on every SIMD one wave issues MFMAs while the other reads LDS and feeds the DMA):
+//   READ slot of phase H: fragment reads (H 0: W n-half 0 and all of X, 16 fragments; H 1:
+//     W n-half 1, 8) + this phase's LDS-DMA pieces, then s_waitcnt vmcnt(<this phase's>);
+//   MMA slot: wait lgkmcnt(0), 32 MFMAs (4 n-tiles x 4 m-tiles x 2 k-steps: 512 cycles).
+// Pieces (16 KB each, 2 buffer_load_dwordx4 ... lds per wave): A = W n-half 0, D = W n-half 1,
+// B / C = the two halves of the X image; A(t+1), B(t+2) issued in phase (t, 0), D(t+1), C(t+2)
+// in phase (t, 1).  X images triple-buffered, W double-buffered: 160 KB of LDS.
+//
+// LDS images, all lane-linear LDS-DMA destinations with the swizzle on the SOURCE address:
+//   NT operand ([rows][64 k], 128-byte rows): 16-byte chunk c of row r at c ^ ((r >> 1) & 7);
+//     the 16x16x32 fragment (row l & 15, k chunk 4 s + (l >> 4)) is one ds_read_b128, and the
+//     four lane groups of the instruction hit 16 distinct bank slots;
+//   k-major operand ([64 k][64 cols] per wave image, 128-byte rows): 32-byte segment s of row
+//     k at s ^ ((k >> 1 & 1) | (k >> 3 & 1) << 1); the fragment (col l & 15, k 8 (l >> 4) + j)
+//     is two ds_read_b64_tr_b16 (4 k rows x 16 cols per 16-lane group), conflict-free.
+// Rows / columns past M or N are clamped onto valid memory; their outputs are not stored.
+//
+// Epilogue: a v_permlane16_swap per accumulator register pair of adjacent n-tiles gives every
+// lane 8 consecutive n of one output row (fp32), so bias / GELU / GELU' read their operands
+// and write the result as 16-byte row pieces; fp32 weight gradients store 16 bytes per
+// register quadruple without a swap.
+#include "gemm_common.h"
+
+namespace orion {
+
+namespace {
+
+constexpr int G_BK = 64, G_IMG = 256 * G_BK;                 // bf16 elements per image
+constexpr int G_X0 = 0, G_W0 = 3 * G_IMG, G_LDS = 5 * G_IMG * 2;  // 160 KB
+
+ORION_DEVICE int nt_swz(int r) { return (r >> 1) & 7; }
+ORION_DEVICE int km_swz(int k) { return ((k >> 1) & 1) | (((k >> 3) & 1) << 1); }
+
+template <int OFF>
+ORION_DEVICE bf16x8 rd_b128(unsigned a) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+
+template <int OFF>
+ORION_DEVICE bf16x4 rd_tr(unsigned a) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+
+ORION_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a),
+                                                 __builtin_bit_cast(bf16x8_mfma, b), c, 0, 0, 0);
+}
+
+ORION_DEVICE void g_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// all fragment reads of the phase retired; the fragments become "+v" operands of the wait so
+// no MFMA that uses them is scheduled above it
+ORION_DEVICE void g_wait_lds(bf16x8 (&a)[4][2], bf16x8 (&b)[4][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]),
+                 "+v"(a[2][1]), "+v"(a[3][0]), "+v"(a[3][1]));
+  asm volatile("" : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]),
+               "+v"(b[2][1]), "+v"(b[3][0]), "+v"(b[3][1]));
+}
+ORION_DEVICE void g_wait_lds(bf16x8 (&a)[4][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]),
+                 "+v"(a[2][1]), "+v"(a[3][0]), "+v"(a[3][1]));
+}
+
+ORION_DEVICE f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+}  // namespace
+
+template <bool XKM, bool WKM, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wv >> 2, wm = wv & 3;
+  const int q = lane >> 4, i16 = lane & 15;
+
+  // work id: bijective XCD remap (blocks of one XCD get a contiguous range of work ids), then
+  // k chunk, then groups of GM m-tiles with the m-tile fastest (the ~32 tiles an XCD runs at
+  // once share GM X panels and ~32 / GM W panels in its L2)
+  constexpr int GM = 4;
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  int w = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tiles_m = (g.M + 255) >> 8, tiles = tiles_m * g.tiles_n;
+  const int kc = w / tiles;
+  w -= kc * tiles;
+  const int grp_sz = GM * g.tiles_n, gidx = w / grp_sz, first_m = gidx * GM;
+  const int gm = min(tiles_m - first_m, GM), in = w - gidx * grp_sz;
+  const int m0 = (first_m + in % gm) * 256, n0 = (in / gm) * 256;
+
+  const int k0 = kc * g.kchunk, kr = min(g.kchunk, g.K - k0);
+  const int nk = kr / G_BK;
+  __amdgpu_buffer_rsrc_t rx, rw;
+  if constexpr (XKM) rx = make_rsrc(g.X + (long)k0 * g.ldx, (unsigned)((long)kr * g.ldx * 2));
+  else rx = make_rsrc(g.X + k0, (unsigned)(((long)g.M * g.ldx - k0) * 2));
+  if constexpr (WKM) rw = make_rsrc(g.W + (long)k0 * g.ldw, (unsigned)((long)kr * g.ldw * 2));
+  else rw = make_rsrc(g.W + k0, (unsigned)(((long)g.N * g.ldw - k0) * 2));
+  const unsigned xstep = XKM ? (unsigned)(G_BK * g.ldx * 2) : G_BK * 2;
+  const unsigned wstep = WKM ? (unsigned)(G_BK * g.ldw * 2) : G_BK * 2;
+
+  // LDS-DMA of piece p (0 A, 1 B, 2 C, 3 D): this wave's blocks e = 0, 1 (one block = 8 image
+  // rows x 128 bytes = one wave instruction: lane -> row lane / 8, 16-byte slot lane % 8)
+  unsigned vo[4][2];
+  int ld[4][2];
+  {
+    const int lr = lane >> 3, slot = lane & 7;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int b = 2 * wm + e;  // 0..7
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {  // X pieces B (jj 0), C (jj 1)
+        if constexpr (XKM) {  // [64 k][64 m] image of wave row block wmp
+          const int wmp = 2 * jj + grp, k = 8 * b + lr;
+          const int m = m0 + wmp * 64 + 8 * (slot ^ (km_swz(k) << 1));
+          vo[1 + jj][e] = (unsigned)(((long)k * g.ldx + min(m, g.M - 8)) * 2);
+          ld[1 + jj][e] = wmp * 4096 + 8 * b * 64;
+        } else {  // [256 m][64 k]: rows wm' 64 + 32 jj + [0, 32)
+          const int row0 = (2 * grp + (b >> 2)) * 64 + jj * 32 + (b & 3) * 8, row = row0 + lr;
+          const int ch = slot ^ nt_swz(row);
+          vo[1 + jj][e] = (unsigned)(((long)min(m0 + row, g.M - 1) * g.ldx + 8 * ch) * 2);
+          ld[1 + jj][e] = row0 * 64;
+        }
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {  // W pieces A (n-half 0), D (n-half 1) of this group
+        const int p = hh ? 3 : 0;
+        if constexpr (WKM) {  // [64 k][64 n] image (grp, hh)
+          const int k = 8 * b + lr;
+          const int col = n0 + grp * 128 + hh * 64 + 8 * (slot ^ (km_swz(k) << 1));
+          vo[p][e] = (unsigned)(((long)k * g.ldw + min(col, g.N - 8)) * 2);
+          ld[p][e] = (2 * grp + hh) * 4096 + 8 * b * 64;
+        } else {  // [256 n][64 k]: rows grp 128 + hh 64 + [0, 64)
+          const int row0 = grp * 128 + hh * 64 + b * 8, row = row0 + lr;
+          const int ch = slot ^ nt_swz(row);
+          vo[p][e] = (unsigned)(((long)min(n0 + row, g.N - 1) * g.ldw + 8 * ch) * 2);
+          ld[p][e] = row0 * 64;
+        }
+      }
+    }
+  }
+  auto ximg = [&](int t) -> bf16_t* { return smem + G_X0 + (t % 3) * G_IMG; };
+  auto wimg = [&](int t) -> bf16_t* { return smem + G_W0 + (t & 1) * G_IMG; };
+  auto issue = [&](int p, int t) {
+    const bool isx = p == 1 || p == 2;
+    bf16_t* base = isx ? ximg(t) : wimg(t);
+    const unsigned so = (unsigned)t * (isx ? xstep : wstep);
+    ORION_DASSERT(t < nk);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) blds16(isx ? rx : rw, vo[p][e], so, base + ld[p][e]);
+  };
+
+  // per-lane fragment offsets (bytes).  NT: row i16 of a 16-row tile, k chunk 4 s + q.
+  // k-major: rows 8 q + (i16 >> 2) (+ 4 for the second read, + 32 for k-step 1), columns
+  // 16 tile + 4 (i16 & 3) with the 32-byte segment (= tile) XOR the row swizzle.
+  int nto[2], kmo[4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) nto[s] = i16 * 128 + (((4 * s + q) ^ nt_swz(i16)) << 4);
+  {
+    const int row0 = 8 * q + (i16 >> 2), h = km_swz(row0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) kmo[b] = row0 * 128 + ((b ^ h) << 5) + 8 * (i16 & 3);
+  }
+  const unsigned lds0 = lds_addr(smem, 0);
+
+  f32x4 acc[8][4];
+  bf16x8 W0[4][2], W1[4][2], X[4][2];  // [tile][k-step]
+
+  // X fragments of k-tile t: the wave's 4 m-tiles
+  auto read_x = [&](int t) {
+    const unsigned base = lds0 + (unsigned)(ximg(t) - smem) * 2 + wm * 8192;
+    if constexpr (XKM) {
+      const unsigned a0 = base + kmo[0], a1 = base + kmo[1], a2 = base + kmo[2], a3 = base + kmo[3];
+      X[0][0] = cat8(rd_tr<0>(a0), rd_tr<512>(a0));
+      X[0][1] = cat8(rd_tr<4096>(a0), rd_tr<4608>(a0));
+      X[1][0] = cat8(rd_tr<0>(a1), rd_tr<512>(a1));
+      X[1][1] = cat8(rd_tr<4096>(a1), rd_tr<4608>(a1));
+      X[2][0] = cat8(rd_tr<0>(a2), rd_tr<512>(a2));
+      X[2][1] = cat8(rd_tr<4096>(a2), rd_tr<4608>(a2));
+      X[3][0] = cat8(rd_tr<0>(a3), rd_tr<512>(a3));
+      X[3][1] = cat8(rd_tr<4096>(a3), rd_tr<4608>(a3));
+    } else {
+      const unsigned a0 = base + nto[0], a1 = base + nto[1];
+      X[0][0] = rd_b128<0>(a0);
+      X[0][1] = rd_b128<0>(a1);
+      X[1][0] = rd_b128<2048>(a0);
+      X[1][1] = rd_b128<2048>(a1);
+      X[2][0] = rd_b128<4096>(a0);
+      X[2][1] = rd_b128<4096>(a1);
+      X[3][0] = rd_b128<6144>(a0);
+      X[3][1] = rd_b128<6144>(a1);
+    }
+  };
+  // W fragments of n-half H of k-tile t: 4 n-tiles
+  auto read_w = [&](bf16x8 (&Wf)[4][2], int t, auto Hc) {
+    constexpr int H = decltype(Hc)::value;
+    if constexpr (WKM) {
+      const unsigned base = lds0 + (unsigned)(wimg(t) - smem) * 2 + (2 * grp + H) * 8192;
+      const unsigned a0 = base + kmo[0], a1 = base + kmo[1], a2 = base + kmo[2], a3 = base + kmo[3];
+      Wf[0][0] = cat8(rd_tr<0>(a0), rd_tr<512>(a0));
+      Wf[0][1] = cat8(rd_tr<4096>(a0), rd_tr<4608>(a0));
+      Wf[1][0] = cat8(rd_tr<0>(a1), rd_tr<512>(a1));
+      Wf[1][1] = cat8(rd_tr<4096>(a1), rd_tr<4608>(a1));
+      Wf[2][0] = cat8(rd_tr<0>(a2), rd_tr<512>(a2));
+      Wf[2][1] = cat8(rd_tr<4096>(a2), rd_tr<4608>(a2));
+      Wf[3][0] = cat8(rd_tr<0>(a3), rd_tr<512>(a3));
+      Wf[3][1] = cat8(rd_tr<4096>(a3), rd_tr<4608>(a3));
+    } else {
+      const unsigned base = lds0 + (unsigned)(wimg(t) - smem) * 2 + grp * 16384 + H * 8192;
+      const unsigned a0 = base + nto[0], a1 = base + nto[1];
+      Wf[0][0] = rd_b128<0>(a0);
+      Wf[0][1] = rd_b128<0>(a1);
+      Wf[1][0] = rd_b128<2048>(a0);
+      Wf[1][1] = rd_b128<2048>(a1);
+      Wf[2][0] = rd_b128<4096>(a0);
+      Wf[2][1] = rd_b128<4096>(a1);
+      Wf[3][0] = rd_b128<6144>(a0);
+      Wf[3][1] = rd_b128<6144>(a1);
+    }
+  };
+
+  // one phase: READ slot (fragments + pieces, then vmcnt(VMN) = this phase's own loads, so
+  // every older piece has landed before the next phase), MMA slot (32 MFMAs)
+  auto phase = [&](auto Hc, auto ISWc, auto ISXc, auto VMNc, int t) {
+    constexpr int H = decltype(Hc)::value, VMN = decltype(VMNc)::value;
+    constexpr bool ISW = decltype(ISWc)::value, ISX = decltype(ISXc)::value;
+    if constexpr (H == 0) {
+      read_w(W0, t, Hc);
+      read_x(t);
+      if constexpr (ISW) issue(0, t + 1);
+      if constexpr (ISX) issue(1, t + 2);
+    } else {
+      read_w(W1, t, Hc);
+      if constexpr (ISW) issue(3, t + 1);
+      if constexpr (ISX) issue(2, t + 2);
+    }
+    wait_vm_exact<VMN>();
+    g_barrier();
+    if constexpr (H == 0) g_wait_lds(W0, X);
+    else g_wait_lds(W1);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 (&Wf)[4][2] = H == 0 ? W0 : W1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][s], X[b][s], acc[4 * H + a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    g_barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
+  using Y = std::true_type;
+  using N = std::false_type;
+
+  // prologue: B0 C0 A0 D0 (B1 C1); phase (0, 0) needs the first three
+  issue(1, 0);
+  issue(2, 0);
+  issue(0, 0);
+  issue(3, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    issue(2, 1);
+    wait_vm_exact<6>();
+  } else {
+    wait_vm_exact<2>();
+  }
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = zero4();
+  g_barrier();
+  if (grp == 1) g_barrier();  // the stagger: group 1 runs one slot behind
+
+  int t = 0;
+  for (; t < nk - 2; ++t) {
+    phase(I0(), Y(), Y(), I4(), t);
+    phase(I1(), Y(), Y(), I4(), t);
+  }
+  if (nk >= 2) {  // t = nk - 2: the W pieces of k-tile nk - 1
+    phase(I0(), Y(), N(), I2(), t);
+    phase(I1(), Y(), N(), I2(), t);
+    ++t;
+  }
+  phase(I0(), N(), N(), I0(), t);
+  phase(I1(), N(), N(), I0(), t);
+  if (grp == 0) g_barrier();  // match group 1's barrier count
+
+  // ------------------------------------------------------------------ epilogue
+  const int mw = m0 + wm * 64;           // this wave's 64-row block
+  const int nw = n0 + grp * 128;         // this wave's 128 columns
+  if constexpr (EPI == EPI_WGRAD) {
+    // fp32 partial tile into slab kc, or the final gradient (fp32 arena or bf16, scaled,
+    // optionally accumulated): register quadruple = 4 consecutive n of row m
+    float* slab = g.ksplit > 1 ? g.slabs + (long)kc * g.M * g.N : nullptr;
+    const float wsc = (g.ksplit == 1 && g.scale) ? *g.scale : 1.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = mw + 16 * b + i16;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int n = nw + 16 * a + 4 * q;
+        if (m < g.M && n < g.N) {
+          const long o = (long)m * g.N + n;
+          f32x4 v = acc[a][b];
+          if (slab) {
+            *reinterpret_cast<f32x4*>(slab + o) = v;
+          } else if (g.out_f32) {
+            f32x4* dst = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) + o);
+            v = v * wsc;
+            if (g.accumulate) v += *dst;
+            *dst = v;
+          } else {
+            bf16x4* dst = reinterpret_cast<bf16x4*>(g.out + o);
+            bf16x4 r, prev;
+            if (g.accumulate) prev = *dst;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = f2bf(v[e] * wsc + (g.accumulate ? bf2f(prev[e]) : 0.f));
+            *dst = r;
+          }
+        }
+      }
+    }
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(g.out, (unsigned)((long)g.M * g.ldo * 2));
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t ro2 = ro;
+  if constexpr (EPI == EPI_BIAS_GELU) ro2 = make_rsrc(g.out2, (unsigned)((long)g.M * g.ldo2 * 2));
+  constexpr bool CS = EPI == EPI_GELU_BWD;
+#pragma unroll
+  for (int ap = 0; ap < 4; ++ap) {
+    // after the swap: lane (q, i16) holds n = nb .. nb + 7 of row m (fp32)
+    const int nb = nw + 16 * (2 * ap + (q & 1)) + 8 * (q >> 1);
+    const bool nok = nb < g.N;
+    const int nc = nok ? nb : 0;
+    [[maybe_unused]] float bias[8];
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+      const bf16x8 b8 = *reinterpret_cast<const bf16x8*>(g.bias + nc);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bias[e] = bf2f(b8[e]);
+    }
+    if constexpr (EPI == EPI_GELU_BWD) {
+      if (g.bias) {
+        const bf16x8 b8 = *reinterpret_cast<const bf16x8*>(g.bias + nc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bias[e] = bf2f(b8[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+      }
+    }
+    [[maybe_unused]] float cs[8];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = mw + 16 * b + i16;
+      const int mc = min(m, g.M - 1);
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * ap][b][r]),
+                                                         __float_as_uint(acc[2 * ap + 1][b][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
+      }
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bias[e];
+      }
+      if constexpr (EPI == EPI_GELU_BWD) {
+        const bf16x8 p8 = *reinterpret_cast<const bf16x8*>(g.pre + (long)mc * g.ldp + nc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad_f(bf2f(p8[e]) + bias[e]);
+      }
+      const bool ok = m < g.M && nok;
+      const unsigned off = ok ? (unsigned)(((long)m * g.ldo + nb) * 2) : 0xFFFFFFF0u;
+      u32x4 pk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+      __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, 0);
+      if constexpr (EPI == EPI_BIAS_GELU) {
+        const unsigned off2 = ok ? (unsigned)(((long)m * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(gelu_tanh_f(v[2 * e]), gelu_tanh_f(v[2 * e + 1]));
+        __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off2, 0, 0);
+      }
+      if constexpr (CS) {
+        const float keep = m < g.M ? 1.f : 0.f;  // rows past M repeat row M - 1
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] = b ? cs[e] + keep * v[e] : keep * v[e];
+      }
+    }
+    if constexpr (CS) {
+      if (g.colsum) {
+        // sum over the 16 lanes of each row group (same n, m = i16): three halving exchange
+        // steps (at offset o a lane keeps the half of its live values selected by lane bit o
+        // and adds its partner's copy of it), then one full add with lane ^ 1; lane i16 ends
+        // with value index (i16 >> 1) & 7
+        auto step = [&](auto Oc) {
+          constexpr int o = decltype(Oc)::value, half = o / 2;
+          const bool up = (i16 & o) != 0;
+#pragma unroll
+          for (int k = 0; k < half; ++k) {
+            const float send = up ? cs[k] : cs[half + k];
+            const float keep = up ? cs[half + k] : cs[k];
+            cs[k] = keep + __shfl_xor(send, o);
+          }
+        };
+        step(std::integral_constant<int, 8>());
+        step(std::integral_constant<int, 4>());
+        step(std::integral_constant<int, 2>());
+        const float tot = cs[0] + __shfl_xor(cs[0], 1);
+        const int n = nb + ((i16 >> 1) & 7);
+        if (!(i16 & 1) && mw < g.M && n < g.N) g.colsum[(long)(mw / 64) * g.N + n] = tot;
+      }
+    }
+  }
+}
+
+template <bool XKM, bool WKM, int EPI>
+static int gemm16_launch(const GemmArgs& a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)gemm16_kernel<XKM, WKM, EPI>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS) != hipSuccess)
+      return -5;
+    attr = true;
+  }
+  const long work = (long)((a.M + 255) / 256) * a.tiles_n * a.ksplit;
+  if (work <= 0 || work > 0x7FFFFFFFL) return -1;
+  gemm16_kernel<XKM, WKM, EPI><<<(unsigned)work, 512, G_LDS, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+int gemm16_wgrad(const GemmArgs& a, hipStream_t st) {
+  return gemm16_launch<true, true, EPI_WGRAD>(a, st);
+}
+
+int gemm16(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
+  GemmArgs a = a0;
+  a.kchunk = a.K;
+  a.ksplit = 1;
+  switch (epi * 2 + (wkm ? 1 : 0)) {
+    case EPI_STORE * 2 + 0: return gemm16_launch<false, false, EPI_STORE>(a, st);
+    case EPI_STORE * 2 + 1: return gemm16_launch<false, true, EPI_STORE>(a, st);
+    case EPI_BIAS * 2 + 0: return gemm16_launch<false, false, EPI_BIAS>(a, st);
+    case EPI_BIAS_GELU * 2 + 0: return gemm16_launch<false, false, EPI_BIAS_GELU>(a, st);
+    case EPI_GELU_BWD * 2 + 1: return gemm16_launch<false, true, EPI_GELU_BWD>(a, st);
+    default: return -4;
+  }
+}
+
+}  // namespace orion

@@ -168,5 +168,9 @@ bool gemm_phased_ok(const GemmArgs& a, int wkm);
 int gemm_phased(const GemmArgs& a, int wkm, int epi, hipStream_t st);
 // weight gradient out[M][N] = sum_k X[k][M] W[k][N] (both operands k-major), split-K
 int gemm_phased_wgrad(const GemmArgs& a, hipStream_t st);
+// csrc/gemm16.hip: the same operations on v_mfma_f32_16x16x32_bf16 (same requirements as
+// gemm_phased_ok, plus 8-element aligned pre-activation rows for EPI_GELU_BWD)
+int gemm16(const GemmArgs& a, int wkm, int epi, hipStream_t st);
+int gemm16_wgrad(const GemmArgs& a, hipStream_t st);
 
 }  // namespace orion

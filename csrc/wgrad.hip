@@ -188,7 +188,8 @@ constexpr int WG_PHASED = 7;
 static int wg_cfg(int M) {
   const char* e = getenv("ORION_WGRAD_CFG");
   int c = e ? atoi(e) : WG_PHASED;
-  if (!(c == WG_PHASED || c == WG_PHASED + 1 || (c >= 0 && c < WG_NCFG))) c = WG_PHASED;
+  if (!(c == WG_PHASED || c == WG_PHASED + 1 || c == WG_PHASED + 2 || (c >= 0 && c < WG_NCFG)))
+    c = WG_PHASED;
   return c >= WG_PHASED && M % 64 ? 0 : c;
 }
 
@@ -256,7 +257,7 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   const int ntiles = t1 * t2;
   if (wg_cfg(M) >= WG_PHASED) {
     GemmArgs a{};
-    a.flags = wg_cfg(M) == WG_PHASED + 1 ? 16 : 0;  // ORION_WGRAD_CFG=8: the 4-quadrant schedule
+    a.flags = wg_cfg(M) == WG_PHASED + 1 ? 16 : 0;  // (9: csrc/gemm16.hip)  // ORION_WGRAD_CFG=8: the 4-quadrant schedule
     a.X = (const bf16_t*)A;  // [M tokens][N1]: the k-major "X" operand, rows of out = N1
     a.ldx = lda;
     a.W = (const bf16_t*)B;  // [M tokens][N2]
@@ -274,6 +275,7 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
     a.accumulate = accumulate;
     a.out_f32 = out_f32;
     if ((long)chunk * (lda > ldb ? lda : ldb) * 2 >= 0xFFFFFF00L) return -1;
+    if (wg_cfg(M) == WG_PHASED + 2) return gemm16_wgrad(a, st);  // ORION_WGRAD_CFG=9
     return gemm_phased_wgrad(a, st);
   }
   const int lds = wgrad_lds(M);

@@ -35,9 +35,17 @@ SHAPES = [(256, 256, 64), (300, 264, 128), (1000, 768, 768), (513, 1000, 192), (
           (4096, 2304, 768), (2048, 3072, 768), (1024, 768, 3072), (777, 50304, 128)]
 
 
+@pytest.fixture(params=["7", "9"], ids=["mfma32", "mfma16"])
+def gemm_cfg(request, monkeypatch):
+    """The phased kernel on v_mfma_f32_32x32x16 (csrc/gemm_phased.hip, 7) and on
+    v_mfma_f32_16x16x32 (csrc/gemm16.hip, 9)."""
+    monkeypatch.setenv("ORION_GEMM_CFG", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("wkm", [False, True])
-def test_gemm_store(M, N, K, wkm):
+def test_gemm_store(M, N, K, wkm, gemm_cfg):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     x = _rnd(g, M, K)
     w = _rnd(g, K, N) if wkm else _rnd(g, N, K)
@@ -48,7 +56,7 @@ def test_gemm_store(M, N, K, wkm):
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES[:6])
-def test_gemm_bias_and_bias_gelu(M, N, K):
+def test_gemm_bias_and_bias_gelu(M, N, K, gemm_cfg):
     g = torch.Generator(device=DEV).manual_seed(7 + M)
     x, w, b = _rnd(g, M, K), _rnd(g, N, K), _rnd(g, N)
     a = x.float() @ w.float().t() + b.float()
@@ -60,7 +68,7 @@ def test_gemm_bias_and_bias_gelu(M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES[:6])
-def test_gemm_gelu_backward_epilogue(M, N, K):
+def test_gemm_gelu_backward_epilogue(M, N, K, gemm_cfg):
     g = torch.Generator(device=DEV).manual_seed(11 + N)
     dy, w, pre = _rnd(g, M, K), _rnd(g, K, N), _rnd(g, M, N)
     out, _ = _C().gemm(dy, w, True, 3, None, pre)
@@ -69,7 +77,7 @@ def test_gemm_gelu_backward_epilogue(M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 768), (4096, 3072, 768), (777, 264, 128)])
-@pytest.mark.parametrize("cfg", ["7", "8", "0"])
+@pytest.mark.parametrize("cfg", ["9", "7", "8", "0"])
 @pytest.mark.parametrize("arena", [None, torch.float32, torch.bfloat16])
 def test_gemm_gelu_bwd_with_bias_grad(M, N, K, cfg, arena, monkeypatch):
     """gemm_gelu_bwd: da = (dy w) * GELU'(pre + b) and db = colsum(da) (per-64-row partials
@@ -132,7 +140,7 @@ def test_gemm_batched_input_shape_and_strided_rows():
 
 @pytest.mark.parametrize("M,N,K", [(300, 264, 128), (1000, 768, 768), (777, 50304, 128)])
 @pytest.mark.parametrize("wkm", [False, True])
-@pytest.mark.parametrize("cfg", ["0", "8"])
+@pytest.mark.parametrize("cfg", ["0", "8", "7", "9"])
 def test_gemm_other_schedules(M, N, K, wkm, cfg, monkeypatch):
     """csrc/gemm.hip's 2-stage kernel (ORION_GEMM_CFG=0) and the phased kernel's 4-quadrant
     schedule (8); the variable is read per call."""
@@ -145,7 +153,7 @@ def test_gemm_other_schedules(M, N, K, wkm, cfg, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768), (8224, 200, 264)])
-@pytest.mark.parametrize("cfg", ["7", "8", "0"])
+@pytest.mark.parametrize("cfg", ["9", "7", "8", "0"])
 @pytest.mark.parametrize("acc", [False, True])
 def test_wgrad_phased_and_two_stage_into_fp32(M, N1, N2, cfg, acc, monkeypatch):
     """Weight gradients on the phased kernel (split-K work items, fp32 slabs) and on
