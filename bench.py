@@ -71,6 +71,10 @@ def parse():
                     help="gradient arena dtype (fp32: accumulation and all-reduce in fp32)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the whole training step in a HIP graph (single GPU)")
+    ap.add_argument("--zero1", action="store_true",
+                    help="ZeRO-1: reduce-scatter gradients, AdamW on this rank's 1/N shard of the "
+                         "fp32 master / Adam state, all-gather the bf16 weights (with one GPU: a "
+                         "world-1 rehearsal of the sharded path)")
     return ap.parse_args()
 
 
@@ -90,6 +94,14 @@ def main():
         dev = launch.device_for(local_rank, local_world, args.dist_backend)
         torch.cuda.set_device(dev)
     rccl_log = None
+    if world == 1 and args.zero1:
+        # a one-rank process group so the sharded optimizer path runs as it would at N > 1
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(launch.free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        launch.init_process_group(args.dist_backend if dev.type == "cuda" else "gloo",
+                                  dev if dev.type == "cuda" and args.dist_backend == "nccl" else None)
     if world > 1:
         if args.dist_backend == "nccl":
             # RCCL's topology / channel INFO log of this rank goes to a file, summarised below
@@ -133,7 +145,7 @@ def main():
     if args.impl == "native":
         trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb, graph=args.hip_graph and world == 1,
                           grad_dtype=torch.float32 if args.grad_dtype == "fp32" else torch.bfloat16,
-                          ddp_timing=world > 1)
+                          ddp_timing=world > 1, zero1=args.zero1)
         step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
     else:
         ddp_model = model
@@ -239,7 +251,10 @@ def main():
             "loss": round(final_loss, 4),
             "max_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
                            if dev.type == "cuda" else None),
-            "dist_backend": args.dist_backend if world > 1 else None,
+            "dist_backend": args.dist_backend if world > 1 or args.zero1 else None,
+            "zero1": bool(args.impl == "native" and trainer.zero1),
+            "optimizer_state_gb_per_rank": (round(3 * 4 * trainer.opt.master.numel() / 2**30, 2)
+                                            if args.impl == "native" else None),
             "allreduce_busbw_gbps": busbw,
             "ddp_buckets": ddp,
             "rccl": rccl,
@@ -249,7 +264,7 @@ def main():
                        "parallelism": f"dp{world}"},
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -366,15 +366,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
 
 using namespace orion;
 
-// ORION_GEMM_CFG: 7 = phase-interleaved kernel (csrc/gemm_phased.hip, default; 8 = its 4-quadrant
+// ORION_GEMM_CFG: 9 = the 16x16x32-MFMA phased kernel (csrc/gemm16.hip, default; round 3: 5-15 %
+// faster than 7 on every GPT-2 / Llama shape measured), 7 = the 32x32x16 phased kernel
+// (csrc/gemm_phased.hip; 8 = its 4-quadrant
 // schedule), 0 = BK 64 x 2 stages, 1 = ping-pong, 2 = BK 32 x 4-stage ring,
 // 3 = BK 32 x 5-stage ring (160 KB: three stages in flight), 4/5/6 = 4 waves of 128 x 128
 // with BK 64 x 2 / BK 32 x 4 / BK 32 x 5 (docs/PERFORMANCE.md, "In-tree GEMM study").
-// 9 = the 16x16x32-MFMA phased kernel (csrc/gemm16.hip).
 static int gemm_cfg() {  // read per call: microbenchmarks switch variants in one process
   const char* e = getenv("ORION_GEMM_CFG");
-  const int c = e ? atoi(e) : 7;
-  return c < 0 || c > 9 ? 7 : c;
+  const int c = e ? atoi(e) : 9;
+  return c < 0 || c > 9 ? 9 : c;
 }
 
 template <bool WKM, int EPI, int BK, int NS, int WM = 4>
@@ -452,7 +453,7 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   const int cfg = gemm_cfg();
   if (cfg == 8) a.flags |= 16;  // phased kernel, SCHED 0 (8-MFMA quadrant phases)
   int rc;
-  if (cfg == 9 && gemm_phased_ok(a, wkm) &&
+  if (cfg == 9 && gemm16_ok(a, wkm) &&
       (epi != EPI_GELU_BWD || (ldp % 8 == 0 && !(reinterpret_cast<uintptr_t>(pre) & 15)))) {
     const int rows = (M + 63) / 64;
     if (db) a.colsum = part;

@@ -73,13 +73,6 @@ ORION_DEVICE void g_barrier() {
 
 // all fragment reads of the phase retired; the fragments become "+v" operands of the wait so
 // no MFMA that uses them is scheduled above it
-ORION_DEVICE void g_wait_lds(bf16x8 (&a)[4][2], bf16x8 (&b)[4][2]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]),
-                 "+v"(a[2][1]), "+v"(a[3][0]), "+v"(a[3][1]));
-  asm volatile("" : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]),
-               "+v"(b[2][1]), "+v"(b[3][0]), "+v"(b[3][1]));
-}
 ORION_DEVICE void g_wait_lds(bf16x8 (&a)[4][2]) {
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]),
@@ -90,13 +83,20 @@ ORION_DEVICE f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 }  // namespace
 
-template <bool XKM, bool WKM, int EPI>
+// STAMPS (diagnostic instantiation: ORION_GEMM_DIAG=4 with a stamp buffer, EPI_STORE only):
+// every wave of every workgroup records s_memtime at 16 points -- kernel start, prologue
+// landed, the 6 slot boundaries of both phases of the middle k-tile (READ start, reads+DMA
+// issued, vmcnt retired, MMA slot entered, fragments landed, MFMAs issued), main loop done,
+// epilogue issued -- into g.slabs as u64 [workgroup][wave][16] (scripts/gemm_stamps.py).
+template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
 __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wv >> 2, wm = wv & 3;
   const int q = lane >> 4, i16 = lane & 15;
+  [[maybe_unused]] unsigned long stp[16];
+  if constexpr (STAMPS) stp[0] = __builtin_amdgcn_s_memtime();
 
   // work id: bijective XCD remap (blocks of one XCD get a contiguous range of work ids), then
   // k chunk, then groups of GM m-tiles with the m-tile fastest (the ~32 tiles an XCD runs at
@@ -114,11 +114,18 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
 
   const int k0 = kc * g.kchunk, kr = min(g.kchunk, g.K - k0);
   const int nk = kr / G_BK;
+  // buffer resources based at this work item's tile (rows m0 / n0) and k chunk, so only the
+  // tile's own extent has to fit the 32-bit offsets (a 6.6 GB logits operand is fine)
+  const int rows_m = min(g.M - m0, 256), rows_n = min(g.N - n0, 256);
   __amdgpu_buffer_rsrc_t rx, rw;
-  if constexpr (XKM) rx = make_rsrc(g.X + (long)k0 * g.ldx, (unsigned)((long)kr * g.ldx * 2));
-  else rx = make_rsrc(g.X + k0, (unsigned)(((long)g.M * g.ldx - k0) * 2));
-  if constexpr (WKM) rw = make_rsrc(g.W + (long)k0 * g.ldw, (unsigned)((long)kr * g.ldw * 2));
-  else rw = make_rsrc(g.W + k0, (unsigned)(((long)g.N * g.ldw - k0) * 2));
+  if constexpr (XKM)
+    rx = make_rsrc(g.X + (long)k0 * g.ldx + m0, (unsigned)(((long)(kr - 1) * g.ldx + rows_m) * 2));
+  else
+    rx = make_rsrc(g.X + (long)m0 * g.ldx + k0, (unsigned)(((long)(rows_m - 1) * g.ldx + kr) * 2));
+  if constexpr (WKM)
+    rw = make_rsrc(g.W + (long)k0 * g.ldw + n0, (unsigned)(((long)(kr - 1) * g.ldw + rows_n) * 2));
+  else
+    rw = make_rsrc(g.W + (long)n0 * g.ldw + k0, (unsigned)(((long)(rows_n - 1) * g.ldw + kr) * 2));
   const unsigned xstep = XKM ? (unsigned)(G_BK * g.ldx * 2) : G_BK * 2;
   const unsigned wstep = WKM ? (unsigned)(G_BK * g.ldw * 2) : G_BK * 2;
 
@@ -136,12 +143,12 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
         if constexpr (XKM) {  // [64 k][64 m] image of wave row block wmp
           const int wmp = 2 * jj + grp, k = 8 * b + lr;
           const int m = m0 + wmp * 64 + 8 * (slot ^ (km_swz(k) << 1));
-          vo[1 + jj][e] = (unsigned)(((long)k * g.ldx + min(m, g.M - 8)) * 2);
+          vo[1 + jj][e] = (unsigned)(((long)k * g.ldx + min(m, g.M - 8) - m0) * 2);
           ld[1 + jj][e] = wmp * 4096 + 8 * b * 64;
         } else {  // [256 m][64 k]: rows wm' 64 + 32 jj + [0, 32)
           const int row0 = (2 * grp + (b >> 2)) * 64 + jj * 32 + (b & 3) * 8, row = row0 + lr;
           const int ch = slot ^ nt_swz(row);
-          vo[1 + jj][e] = (unsigned)(((long)min(m0 + row, g.M - 1) * g.ldx + 8 * ch) * 2);
+          vo[1 + jj][e] = (unsigned)(((long)(min(m0 + row, g.M - 1) - m0) * g.ldx + 8 * ch) * 2);
           ld[1 + jj][e] = row0 * 64;
         }
       }
@@ -151,12 +158,12 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
         if constexpr (WKM) {  // [64 k][64 n] image (grp, hh)
           const int k = 8 * b + lr;
           const int col = n0 + grp * 128 + hh * 64 + 8 * (slot ^ (km_swz(k) << 1));
-          vo[p][e] = (unsigned)(((long)k * g.ldw + min(col, g.N - 8)) * 2);
+          vo[p][e] = (unsigned)(((long)k * g.ldw + min(col, g.N - 8) - n0) * 2);
           ld[p][e] = (2 * grp + hh) * 4096 + 8 * b * 64;
         } else {  // [256 n][64 k]: rows grp 128 + hh 64 + [0, 64)
           const int row0 = grp * 128 + hh * 64 + b * 8, row = row0 + lr;
           const int ch = slot ^ nt_swz(row);
-          vo[p][e] = (unsigned)(((long)min(n0 + row, g.N - 1) * g.ldw + 8 * ch) * 2);
+          vo[p][e] = (unsigned)(((long)(min(n0 + row, g.N - 1) - n0) * g.ldw + 8 * ch) * 2);
           ld[p][e] = row0 * 64;
         }
       }
@@ -187,47 +194,38 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   const unsigned lds0 = lds_addr(smem, 0);
 
   f32x4 acc[8][4];
-  bf16x8 W0[4][2], W1[4][2], X[4][2];  // [tile][k-step]
+  // fragments: W [tile][k-step] (n-half 0 / 1), X [m-tile] of k-step 0 and of k-step 1
+  bf16x8 W0[4][2], W1[4][2], X0[4], X1[4];
 
-  // X fragments of k-tile t: the wave's 4 m-tiles
-  auto read_x = [&](int t) {
+  // the wave's 4 m-tile fragments of k-step s of k-tile t
+  auto read_x = [&](bf16x8 (&Xd)[4], int t, auto Sc) {
+    constexpr int S = decltype(Sc)::value;
     const unsigned base = lds0 + (unsigned)(ximg(t) - smem) * 2 + wm * 8192;
     if constexpr (XKM) {
-      const unsigned a0 = base + kmo[0], a1 = base + kmo[1], a2 = base + kmo[2], a3 = base + kmo[3];
-      X[0][0] = cat8(rd_tr<0>(a0), rd_tr<512>(a0));
-      X[0][1] = cat8(rd_tr<4096>(a0), rd_tr<4608>(a0));
-      X[1][0] = cat8(rd_tr<0>(a1), rd_tr<512>(a1));
-      X[1][1] = cat8(rd_tr<4096>(a1), rd_tr<4608>(a1));
-      X[2][0] = cat8(rd_tr<0>(a2), rd_tr<512>(a2));
-      X[2][1] = cat8(rd_tr<4096>(a2), rd_tr<4608>(a2));
-      X[3][0] = cat8(rd_tr<0>(a3), rd_tr<512>(a3));
-      X[3][1] = cat8(rd_tr<4096>(a3), rd_tr<4608>(a3));
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const unsigned a = base + kmo[b];
+        Xd[b] = cat8(rd_tr<4096 * S>(a), rd_tr<4096 * S + 512>(a));
+      }
     } else {
-      const unsigned a0 = base + nto[0], a1 = base + nto[1];
-      X[0][0] = rd_b128<0>(a0);
-      X[0][1] = rd_b128<0>(a1);
-      X[1][0] = rd_b128<2048>(a0);
-      X[1][1] = rd_b128<2048>(a1);
-      X[2][0] = rd_b128<4096>(a0);
-      X[2][1] = rd_b128<4096>(a1);
-      X[3][0] = rd_b128<6144>(a0);
-      X[3][1] = rd_b128<6144>(a1);
+      const unsigned a = base + nto[S];
+      Xd[0] = rd_b128<0>(a);
+      Xd[1] = rd_b128<2048>(a);
+      Xd[2] = rd_b128<4096>(a);
+      Xd[3] = rd_b128<6144>(a);
     }
   };
-  // W fragments of n-half H of k-tile t: 4 n-tiles
+  // W fragments of n-half H of k-tile t: 4 n-tiles x 2 k-steps
   auto read_w = [&](bf16x8 (&Wf)[4][2], int t, auto Hc) {
     constexpr int H = decltype(Hc)::value;
     if constexpr (WKM) {
       const unsigned base = lds0 + (unsigned)(wimg(t) - smem) * 2 + (2 * grp + H) * 8192;
-      const unsigned a0 = base + kmo[0], a1 = base + kmo[1], a2 = base + kmo[2], a3 = base + kmo[3];
-      Wf[0][0] = cat8(rd_tr<0>(a0), rd_tr<512>(a0));
-      Wf[0][1] = cat8(rd_tr<4096>(a0), rd_tr<4608>(a0));
-      Wf[1][0] = cat8(rd_tr<0>(a1), rd_tr<512>(a1));
-      Wf[1][1] = cat8(rd_tr<4096>(a1), rd_tr<4608>(a1));
-      Wf[2][0] = cat8(rd_tr<0>(a2), rd_tr<512>(a2));
-      Wf[2][1] = cat8(rd_tr<4096>(a2), rd_tr<4608>(a2));
-      Wf[3][0] = cat8(rd_tr<0>(a3), rd_tr<512>(a3));
-      Wf[3][1] = cat8(rd_tr<4096>(a3), rd_tr<4608>(a3));
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const unsigned ad = base + kmo[a];
+        Wf[a][0] = cat8(rd_tr<0>(ad), rd_tr<512>(ad));
+        Wf[a][1] = cat8(rd_tr<4096>(ad), rd_tr<4608>(ad));
+      }
     } else {
       const unsigned base = lds0 + (unsigned)(wimg(t) - smem) * 2 + grp * 16384 + H * 8192;
       const unsigned a0 = base + nto[0], a1 = base + nto[1];
@@ -241,15 +239,29 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
       Wf[3][1] = rd_b128<6144>(a1);
     }
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
+  using Y = std::true_type;
+  using N = std::false_type;
 
+  [[maybe_unused]] const int tsel = nk / 2;
+  auto stamp = [&](int t, int k) {
+    if constexpr (STAMPS) {
+      if (t == tsel) stp[k] = __builtin_amdgcn_s_memtime();
+    }
+  };
   // one phase: READ slot (fragments + pieces, then vmcnt(VMN) = this phase's own loads, so
   // every older piece has landed before the next phase), MMA slot (32 MFMAs)
   auto phase = [&](auto Hc, auto ISWc, auto ISXc, auto VMNc, int t) {
     constexpr int H = decltype(Hc)::value, VMN = decltype(VMNc)::value;
     constexpr bool ISW = decltype(ISWc)::value, ISX = decltype(ISXc)::value;
+    stamp(t, 2 + 6 * H);
     if constexpr (H == 0) {
       read_w(W0, t, Hc);
-      read_x(t);
+      read_x(X0, t, I0());
+      read_x(X1, t, I1());
       if constexpr (ISW) issue(0, t + 1);
       if constexpr (ISX) issue(1, t + 2);
     } else {
@@ -257,28 +269,35 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
       if constexpr (ISW) issue(3, t + 1);
       if constexpr (ISX) issue(2, t + 2);
     }
+    stamp(t, 3 + 6 * H);
     wait_vm_exact<VMN>();
+    stamp(t, 4 + 6 * H);
     g_barrier();
-    if constexpr (H == 0) g_wait_lds(W0, X);
-    else g_wait_lds(W1);
+    stamp(t, 5 + 6 * H);
+    // every fragment an MFMA of this slot reads is retired (and pinned behind the wait)
+    if constexpr (H == 0) {
+      g_wait_lds(W0);
+      asm volatile("" : "+v"(X0[0]), "+v"(X0[1]), "+v"(X0[2]), "+v"(X0[3]), "+v"(X1[0]),
+                   "+v"(X1[1]), "+v"(X1[2]), "+v"(X1[3]));
+    } else {
+      g_wait_lds(W1);
+    }
     __builtin_amdgcn_sched_barrier(0);
+    stamp(t, 6 + 6 * H);
     bf16x8 (&Wf)[4][2] = H == 0 ? W0 : W1;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][0], X0[b], acc[4 * H + a][b]);
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][s], X[b][s], acc[4 * H + a][b]);
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][1], X1[b], acc[4 * H + a][b]);
     __builtin_amdgcn_s_setprio(0);
+    stamp(t, 7 + 6 * H);
     g_barrier();
   };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I4 = std::integral_constant<int, 4>;
-  using Y = std::true_type;
-  using N = std::false_type;
 
   // prologue: B0 C0 A0 D0 (B1 C1); phase (0, 0) needs the first three
   issue(1, 0);
@@ -292,6 +311,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   } else {
     wait_vm_exact<2>();
   }
+  if constexpr (STAMPS) stp[1] = __builtin_amdgcn_s_memtime();
 #pragma unroll
   for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -299,12 +319,14 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   g_barrier();
   if (grp == 1) g_barrier();  // the stagger: group 1 runs one slot behind
 
+  // steady state: k-tiles 0 .. nk - 3 issue pieces of t + 1 and t + 2; k-tile nk - 2 issues
+  // the W pieces of nk - 1; k-tile nk - 1 issues nothing
   int t = 0;
   for (; t < nk - 2; ++t) {
     phase(I0(), Y(), Y(), I4(), t);
     phase(I1(), Y(), Y(), I4(), t);
   }
-  if (nk >= 2) {  // t = nk - 2: the W pieces of k-tile nk - 1
+  if (nk >= 2) {
     phase(I0(), Y(), N(), I2(), t);
     phase(I1(), Y(), N(), I2(), t);
     ++t;
@@ -312,6 +334,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   phase(I0(), N(), N(), I0(), t);
   phase(I1(), N(), N(), I0(), t);
   if (grp == 0) g_barrier();  // match group 1's barrier count
+  if constexpr (STAMPS) stp[14] = __builtin_amdgcn_s_memtime();
 
   // ------------------------------------------------------------------ epilogue
   const int mw = m0 + wm * 64;           // this wave's 64-row block
@@ -350,9 +373,12 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
     }
     return;
   }
-  const __amdgpu_buffer_rsrc_t ro = make_rsrc(g.out, (unsigned)((long)g.M * g.ldo * 2));
+  // output resources based at row m0 (32-bit offsets cover one 256-row band)
+  const __amdgpu_buffer_rsrc_t ro =
+      make_rsrc(g.out + (long)m0 * g.ldo, (unsigned)(((long)(rows_m - 1) * g.ldo + g.N) * 2));
   [[maybe_unused]] __amdgpu_buffer_rsrc_t ro2 = ro;
-  if constexpr (EPI == EPI_BIAS_GELU) ro2 = make_rsrc(g.out2, (unsigned)((long)g.M * g.ldo2 * 2));
+  if constexpr (EPI == EPI_BIAS_GELU)
+    ro2 = make_rsrc(g.out2 + (long)m0 * g.ldo2, (unsigned)(((long)(rows_m - 1) * g.ldo2 + g.N) * 2));
   constexpr bool CS = EPI == EPI_GELU_BWD;
 #pragma unroll
   for (int ap = 0; ap < 4; ++ap) {
@@ -399,13 +425,13 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
         for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad_f(bf2f(p8[e]) + bias[e]);
       }
       const bool ok = m < g.M && nok;
-      const unsigned off = ok ? (unsigned)(((long)m * g.ldo + nb) * 2) : 0xFFFFFFF0u;
+      const unsigned off = ok ? (unsigned)(((long)(m - m0) * g.ldo + nb) * 2) : 0xFFFFFFF0u;
       u32x4 pk;
 #pragma unroll
       for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
       __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, 0);
       if constexpr (EPI == EPI_BIAS_GELU) {
-        const unsigned off2 = ok ? (unsigned)(((long)m * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
+        const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(gelu_tanh_f(v[2 * e]), gelu_tanh_f(v[2 * e + 1]));
         __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off2, 0, 0);
@@ -441,21 +467,42 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
       }
     }
   }
+  if constexpr (STAMPS) {
+    stp[15] = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      unsigned long* dst = reinterpret_cast<unsigned long*>(g.slabs) + ((long)blockIdx.x * 8 + wv) * 16;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) dst[k] = stp[k];
+    }
+  }
 }
 
-template <bool XKM, bool WKM, int EPI>
+template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
 static int gemm16_launch(const GemmArgs& a, hipStream_t st) {
+  if constexpr (!STAMPS && EPI == EPI_STORE) {
+    if ((a.flags & 4) && a.slabs) return gemm16_launch<XKM, WKM, EPI, true>(a, st);
+  }
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm16_kernel<XKM, WKM, EPI>,
+    if (hipFuncSetAttribute((const void*)gemm16_kernel<XKM, WKM, EPI, STAMPS>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS) != hipSuccess)
       return -5;
     attr = true;
   }
   const long work = (long)((a.M + 255) / 256) * a.tiles_n * a.ksplit;
   if (work <= 0 || work > 0x7FFFFFFFL) return -1;
-  gemm16_kernel<XKM, WKM, EPI><<<(unsigned)work, 512, G_LDS, st>>>(a);
+  gemm16_kernel<XKM, WKM, EPI, STAMPS><<<(unsigned)work, 512, G_LDS, st>>>(a);
   return (int)hipGetLastError();
+}
+
+// 32-bit buffer offsets of one work item: a k-major operand spans its whole k chunk, an NT
+// operand and the output one 256-row band
+bool gemm16_ok(const GemmArgs& a, int wkm) {
+  const long lim = 0xFFFFFF00L;
+  const long band = 256L * (a.ldx > a.ldw ? a.ldx : a.ldw) * 2;
+  const long ob = 256L * (a.ldo > a.ldo2 ? a.ldo : a.ldo2) * 2;
+  const long wb = wkm ? (long)a.K * a.ldw * 2 : 0;
+  return band < lim && ob < lim && wb < lim;
 }
 
 int gemm16_wgrad(const GemmArgs& a, hipStream_t st) {

@@ -170,6 +170,7 @@ int gemm_phased(const GemmArgs& a, int wkm, int epi, hipStream_t st);
 int gemm_phased_wgrad(const GemmArgs& a, hipStream_t st);
 // csrc/gemm16.hip: the same operations on v_mfma_f32_16x16x32_bf16 (same requirements as
 // gemm_phased_ok, plus 8-element aligned pre-activation rows for EPI_GELU_BWD)
+bool gemm16_ok(const GemmArgs& a, int wkm);
 int gemm16(const GemmArgs& a, int wkm, int epi, hipStream_t st);
 int gemm16_wgrad(const GemmArgs& a, hipStream_t st);
 

@@ -180,16 +180,18 @@ struct WgCfg { int ks, ns, wm; };
 constexpr WgCfg WG_CFGS[] = {{2, 4, 4}, {2, 4, 2}, {4, 2, 2}, {2, 2, 4}};
 constexpr int WG_NCFG = sizeof(WG_CFGS) / sizeof(WG_CFGS[0]);
 
-// ORION_WGRAD_CFG: 7 = the phase-interleaved kernel (csrc/gemm_phased.hip, default), 0-3 =
+// ORION_WGRAD_CFG: 9 = the 16x16x32-MFMA phased kernel (csrc/gemm16.hip, default: GPT-2 weight
+// gradients 4.9 vs 5.6 ms, whole step +3.9 %), 7 = the 32x32x16 phased kernel
+// (csrc/gemm_phased.hip), 0-3 =
 // wgrad_kernel configurations of WG_CFGS (read per call: microbenchmarks switch in-process)
 constexpr int WG_PHASED = 7;
 // (the phased kernel stages 64-token k-tiles: token counts that are not a multiple of 64
 // take wgrad_kernel's default configuration, which stages 32)
 static int wg_cfg(int M) {
   const char* e = getenv("ORION_WGRAD_CFG");
-  int c = e ? atoi(e) : WG_PHASED;
+  int c = e ? atoi(e) : WG_PHASED + 2;
   if (!(c == WG_PHASED || c == WG_PHASED + 1 || c == WG_PHASED + 2 || (c >= 0 && c < WG_NCFG)))
-    c = WG_PHASED;
+    c = WG_PHASED + 2;
   return c >= WG_PHASED && M % 64 ? 0 : c;
 }
 

@@ -91,8 +91,8 @@ class MLP(nn.Module):
         self.dropout = cfg.dropout
 
     def forward(self, x, fuse_out_bias=False):
-        y = ops.gelu_linear(ops.linear(x, self.c_fc.weight), self.c_fc.bias, self.c_proj.weight,
-                            None if fuse_out_bias else self.c_proj.bias)
+        y = ops.mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight,
+                    None if fuse_out_bias else self.c_proj.bias)
         if self.dropout and self.training:
             y = F.dropout(y, self.dropout)
         return y

@@ -133,6 +133,18 @@ def gelu_linear(a, fc_bias, weight, bias=None):
     return linear(h, weight, bias)
 
 
+def mlp(x, w_fc, b_fc, w_proj, b_proj=None):
+    """GPT-2's MLP: linear(gelu(x W_fc^T + b_fc), W_proj, b_proj).  On the GPT-2 GPU path
+    (``ORION_FUSED_MLP``) both GELU passes live in GEMM epilogues (ops/activations.py
+    ``_FusedMLP``); otherwise the fc GEMM then :func:`gelu_linear`."""
+    b = _gpu(x)
+    if b == "hip":
+        from .activations import mlp_hip, mlp_ok
+        if mlp_ok(x, w_fc, w_proj):
+            return mlp_hip(x, w_fc, b_fc, w_proj, b_proj)
+    return gelu_linear(linear(x, w_fc), b_fc, w_proj, b_proj)
+
+
 def swiglu(gate_up):
     """silu(gate) * up on a packed (..., 2F) [gate | up] projection -> (..., F)."""
     b = _gpu(gate_up)

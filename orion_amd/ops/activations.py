@@ -1,5 +1,7 @@
-"""GELU(+bias) and SwiGLU autograd wrappers over csrc/activations.hip, and the fused MLP tail
-linear(gelu(a + b_fc)) whose backward is one GEMM (csrc/gemm_phased.hip, EPI_GELU_BWD)."""
+"""GELU(+bias) and SwiGLU autograd wrappers over csrc/activations.hip, the fused MLP tail
+linear(gelu(a + b_fc)) whose backward is one GEMM (EPI_GELU_BWD), and the fully fused GPT-2
+MLP (``mlp_hip``): bias + GELU in the fc GEMM's epilogue, GELU' + the fc-bias gradient in
+the projection's input-gradient GEMM (csrc/gemm16.hip) -- no separate GELU pass either way."""
 from __future__ import annotations
 
 import os
@@ -7,7 +9,7 @@ import os
 import torch
 
 from ._ext import C
-from .gemm import linear_fwd, wgrad, wgrad_into
+from .gemm import EPI_BIAS_GELU, linear_dgrad, linear_fwd, wgrad, wgrad_into
 from .grad_sink import sink_of
 from .layernorm import _claim, _notify, _unless, _view
 
@@ -120,3 +122,82 @@ class _GeluLinear(torch.autograd.Function):
 
 def gelu_linear_hip(a, b_fc, weight, bias=None):
     return _GeluLinear.apply(a, b_fc, weight, bias)
+
+
+# ORION_FUSED_MLP=1 (see _FusedMLP): the GPT-2 MLP with both GELU passes inside GEMM epilogues
+def mlp_ok(x, w_fc, w_proj) -> bool:
+    C_ = x.shape[-1]
+    return (_FUSED_MLP and x.dtype == torch.bfloat16 and w_fc.dtype == torch.bfloat16
+            and w_proj.dtype == torch.bfloat16 and x.is_contiguous() and w_fc.is_contiguous()
+            and w_proj.is_contiguous() and C_ % 64 == 0 and w_fc.shape[0] % 64 == 0
+            and w_fc.shape[0] % 8 == 0 and w_proj.shape[0] % 8 == 0
+            and x.data_ptr() % 16 == 0 and w_fc.data_ptr() % 16 == 0 and w_proj.data_ptr() % 16 == 0)
+
+
+class _FusedMLP(torch.autograd.Function):
+    """y = gelu(x W_fc^T + b_fc) W_proj^T (+ b_proj), GPT-2's MLP (GELU-tanh
+    fused with the bias add), as GEMMs only:
+
+    forward   (a, h) = one in-tree GEMM x W_fc^T whose epilogue adds b_fc and writes both the
+              pre-activation a and h = gelu(a) (EPI_BIAS_GELU); y = h W_proj^T;
+    backward  (da, db_fc) = one in-tree GEMM dy W_proj whose epilogue multiplies by GELU'(a)
+              and emits the column sums of da (EPI_GELU_BWD); dW_proj = dy^T h,
+              dx = da W_fc, dW_fc = da^T x (weight gradients straight into the arena).
+
+    Against the unfused bias_gelu -> linear pair this drops two (M, 4C) HBM passes per layer
+    (the GELU forward and backward kernels) and the separate fc-bias column sum."""
+
+    @staticmethod
+    def forward(ctx, x, w_fc, b_fc, w_proj, b_proj):
+        C_ = x.shape[-1]
+        x2 = x.reshape(-1, C_)
+        bb = None if b_fc is None else b_fc.to(torch.bfloat16)
+        if bb is None:
+            a = linear_fwd(x2, w_fc)
+            h = C().bias_gelu_fwd(a, None).view(a.shape)
+        else:
+            a, h = C().gemm(x2, w_fc, False, EPI_BIAS_GELU, bb, None)
+        y = linear_fwd(h, w_proj, b_proj)
+        ctx.save_for_backward(x2, a, h, w_fc, w_proj)
+        ctx.biases = (b_fc, b_proj)
+        ctx.sinks = (sink_of(w_fc), sink_of(w_proj))
+        ctx.x_shape = x.shape
+        return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, a, h, w_fc, w_proj = ctx.saved_tensors
+        b_fc, b_proj = ctx.biases
+        s_fc, s_proj = ctx.sinks
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        sbfc, sbproj = _claim((b_fc, b_proj))
+        # a already holds the fc bias: GELU'(a), no bias operand
+        da, dbfc = C().gemm_gelu_bwd(dy2, w_proj, a, None, _view(sbfc))
+        _notify(sbfc)
+        dbfc = None if b_fc is None else _unless(dbfc, sbfc)
+        grads = [None, None, None, None, None]
+        if ctx.needs_input_grad[3]:
+            if s_proj is not None:
+                wgrad_into(dy2, h, s_proj.view, s_proj.take())
+                s_proj.notify()
+            else:
+                grads[3] = wgrad(dy2, h)
+        if b_proj is not None and ctx.needs_input_grad[4]:
+            db = C().colsum(dy2, _view(sbproj))
+            grads[4] = None if sbproj is not None else db.to(b_proj.dtype)
+            _notify(sbproj)
+        if ctx.needs_input_grad[0]:
+            grads[0] = linear_dgrad(da, w_fc).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            if s_fc is not None:
+                wgrad_into(da, x2, s_fc.view, s_fc.take())
+                s_fc.notify()
+            else:
+                grads[1] = wgrad(da, x2)
+        if dbfc is not None:
+            grads[2] = dbfc.to(b_fc.dtype)
+        return tuple(grads)
+
+
+def mlp_hip(x, w_fc, b_fc, w_proj, b_proj=None):
+    return _FusedMLP.apply(x, w_fc, b_fc, w_proj, b_proj)

@@ -29,14 +29,11 @@ from ._ext import C
 from .determinism import deterministic
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
-# Linear-layer forward (x W^T [+ b]) and input gradient (dy W).  ORION_GEMM=blas (default):
-# hipBLASLt.  ORION_GEMM=auto: the in-tree phased kernel (csrc/gemm_phased.hip) for the input
-# gradients it wins in isolation -- narrow outputs (N <= 1024) over K <= 8192 with >= 256
-# output tiles: the GPT-2 qkv / attn-proj / fc dgrads run 5-18 % faster than hipBLASLt
-# (profiles/gemm_study/bench_sched1_vs_blas_gpt2.log) -- but the whole GPT-2 step measured
-# 996.6k vs 1000.1k tok/s (3 alternating runs each), so it is not the default; hipBLASLt
-# keeps the forward shapes, the LM head and Llama-7B's wide shapes (1-35 % faster there).
-# ORION_GEMM=hip routes every eligible GEMM in-tree.  Inside a HIP-graph capture (``hip_gemms()``)
+# Linear-layer forward (x W^T [+ b]) and input gradient (dy W).  ORION_GEMM=blas: hipBLASLt.
+# ORION_GEMM=auto: every input gradient on the in-tree 16x16x32-MFMA kernel (csrc/gemm16.hip:
+# the GPT-2 qkv / attn-proj / fc dgrads run 8-25 % faster than hipBLASLt in isolation,
+# profiles/gemm16/), forward GEMMs on hipBLASLt.  ORION_GEMM=hip routes every eligible GEMM
+# in-tree.  Inside a HIP-graph capture (``hip_gemms()``)
 # every eligible GEMM is in-tree (no library-side host state between replays), and so in the
 # deterministic mode (ops/determinism.py): one workgroup per output tile, no split-K.
 _GEMM_IMPL = os.environ.get("ORION_GEMM", "blas")  # "blas" | "auto" | "hip"
@@ -66,11 +63,7 @@ def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
 
 
 def _hip_wins(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
-    if not w_kmajor:
-        return False
-    K, N = x.shape[-1], w.shape[1]
-    M = x.numel() // K
-    return N <= 1024 and K <= 8192 and M * N >= 256 * 256 * 256
+    return w_kmajor
 
 
 def use_hip_gemm(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:

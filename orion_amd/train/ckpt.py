@@ -25,11 +25,13 @@ def model_type_of(model):
     return "llama" if isinstance(model, Llama) else "gpt2"
 
 
-def save_checkpoint(path, trainer, best_val_loss=None, config=None):
+def save_checkpoint(path, trainer, best_val_loss=None, config=None, write=True):
+    """nanoGPT layout.  Under ZeRO-1 the master weights and Adam moments are gathered from
+    the shards (a collective: every rank calls this, ``write`` only on one)."""
     model = trainer.model
     opt = trainer.opt
     sd = {}
-    master = opt.master
+    master = trainer.full_master()
     for s in trainer.arena.slots:
         sd[s.name] = master[s.offset:s.offset + s.numel].view(s.param.shape).detach().float().cpu().clone()
     # tied weights appear once in the arena; restore every alias name
@@ -39,6 +41,16 @@ def save_checkpoint(path, trainer, best_val_loss=None, config=None):
                 if s.param is p:
                     sd[name] = sd[s.name]
     osd = opt.state_dict()
+    moments = {}
+    for k in ("exp_avg", "exp_avg_sq"):
+        full = trainer.reducer.gather_full(osd[k]) if getattr(trainer, "zero1", False) else osd[k]
+        # per parameter name, so a checkpoint restores into any arena layout (ZeRO-1 padding,
+        # another world size)
+        moments[k] = {s.name: full[s.offset:s.offset + s.numel].detach().cpu().clone()
+                      for s in trainer.arena.slots}
+    osd.update(moments)
+    if not write:
+        return path
     ckpt = {
         "model": sd,
         "optimizer": {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in osd.items()
@@ -75,14 +87,32 @@ def build_model_from_checkpoint(ckpt):
 
 
 def restore_trainer(trainer, ckpt):
-    """Load master weights + Adam state into an existing Trainer (resume)."""
+    """Load master weights + Adam state into an existing Trainer (resume); under ZeRO-1 each
+    rank keeps its shard of them."""
     opt = trainer.opt
     sd = ckpt["model"]
+    zero1 = getattr(trainer, "zero1", False)
     with torch.no_grad():
+        full = torch.zeros(trainer.arena.numel, dtype=torch.float32, device=opt.master.device) \
+            if zero1 else opt.master
         for s in trainer.arena.slots:
-            opt.master[s.offset:s.offset + s.numel].copy_(sd[s.name].reshape(-1))
+            full[s.offset:s.offset + s.numel].copy_(sd[s.name].reshape(-1))
         o = dict(ckpt["optimizer"])
-        o["master"] = opt.master
-        opt.load_state_dict(o)
+        for k in ("exp_avg", "exp_avg_sq"):
+            if isinstance(o[k], dict):  # per-name moments -> this trainer's arena layout
+                flat = torch.zeros(trainer.arena.numel, dtype=torch.float32, device=full.device)
+                for s in trainer.arena.slots:
+                    flat[s.offset:s.offset + s.numel].copy_(o[k][s.name].reshape(-1))
+                o[k] = flat
+        if zero1:
+            shard = trainer.reducer.shard_of
+            o["exp_avg"] = shard(o["exp_avg"].to(full.device))
+            o["exp_avg_sq"] = shard(o["exp_avg_sq"].to(full.device))
+            o["master"] = shard(full)
+            opt.load_state_dict(o)
+            trainer.reducer.gather_params()
+        else:
+            o["master"] = opt.master
+            opt.load_state_dict(o)
     trainer.iter_num = int(ckpt.get("iter_num", 0))
     return trainer

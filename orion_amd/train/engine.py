@@ -69,7 +69,8 @@ class Trainer:
 
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float | None = None, arena_dtype=None,
-                 graph: bool = False, grad_dtype=None, ddp_timing: bool = False):
+                 graph: bool = False, grad_dtype=None, ddp_timing: bool = False,
+                 zero1: bool = False):
         self.model = model
         self.cfg = optim or OptimConfig()
         dev = next(model.parameters()).device
@@ -80,20 +81,41 @@ class Trainer:
             # precision; ORION_GRAD_DTYPE=bf16 opts into the all-bf16 arena
             grad_dtype = (torch.bfloat16 if os.environ.get("ORION_GRAD_DTYPE") == "bf16"
                           else torch.float32)
-        self.arena = FlatArena(model, dtype=arena_dtype, grad_dtype=grad_dtype)
-        self.opt = FlatAdamW(self.arena, lr=self.cfg.learning_rate,
-                             betas=(self.cfg.beta1, self.cfg.beta2),
-                             weight_decay=self.cfg.weight_decay, grad_clip=self.cfg.grad_clip)
         if ddp is None:
             ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        # ZeRO-1 (parallel/ddp.py ShardedGradReducer): reduce-scatter the gradient buckets, AdamW
+        # on this rank's 1/N shard of master / m / v, all-gather the bf16 weights.  Also valid
+        # with one rank (a rehearsal of the sharded code path).
+        self.zero1 = bool(zero1) and dist.is_available() and dist.is_initialized()
         self.reducer = None
-        if ddp:
-            from ..parallel.ddp import GradBucketReducer
-            self.reducer = GradBucketReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing)
+        if self.zero1:
+            from ..parallel.ddp import ShardedGradReducer, zero1_pad_names
+            names, pad_to = zero1_pad_names(model, bucket_mb, grad_dtype, dist.get_world_size())
+            self.arena = FlatArena(model, dtype=arena_dtype, grad_dtype=grad_dtype,
+                                   pad_after=names, pad_to=pad_to)
             # R1: every rank starts from rank 0's exact fp32 weights
-            dist.broadcast(self.opt.master, 0)
+            dist.broadcast(self.arena.init_fp32, 0)
             with torch.no_grad():
-                self.arena.params.copy_(self.opt.master)
+                self.arena.params.copy_(self.arena.init_fp32)
+            self.reducer = ShardedGradReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing)
+            self.reducer.init_fp32 = self.reducer.shard_of(self.arena.init_fp32)
+            self.arena.init_fp32 = None
+            self.opt = FlatAdamW(self.reducer, lr=self.cfg.learning_rate,
+                                 betas=(self.cfg.beta1, self.cfg.beta2),
+                                 weight_decay=self.cfg.weight_decay, grad_clip=self.cfg.grad_clip)
+            self.opt.sumsq_hook = self.reducer.reduce_sumsq
+        else:
+            self.arena = FlatArena(model, dtype=arena_dtype, grad_dtype=grad_dtype)
+            self.opt = FlatAdamW(self.arena, lr=self.cfg.learning_rate,
+                                 betas=(self.cfg.beta1, self.cfg.beta2),
+                                 weight_decay=self.cfg.weight_decay, grad_clip=self.cfg.grad_clip)
+            if ddp:
+                from ..parallel.ddp import GradBucketReducer
+                self.reducer = GradBucketReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing)
+                # R1: every rank starts from rank 0's exact fp32 weights
+                dist.broadcast(self.opt.master, 0)
+                with torch.no_grad():
+                    self.arena.params.copy_(self.opt.master)
         self.iter_num = 0
         self.graph_enabled = bool(graph) and dev.type == "cuda" and self.reducer is None
         self._graph = None
@@ -127,6 +149,8 @@ class Trainer:
         if self.reducer is not None:
             self.reducer.finish()
         self.opt.step()
+        if self.zero1:
+            self.reducer.gather_params()
         self.iter_num += 1
         return torch.stack(losses).mean()
 
@@ -179,6 +203,10 @@ class Trainer:
         self.iter_num += 1
         return self._static_loss
 
+    def full_master(self):
+        """fp32 master weights in arena layout (gathered from the shards under ZeRO-1)."""
+        return self.reducer.gather_full(self.opt.master) if self.zero1 else self.opt.master
+
     def state_dict(self):
-        return dict(model=self.arena.state_dict_fp32(self.opt.master),
+        return dict(model=self.arena.state_dict_fp32(self.full_master()),
                     optimizer=self.opt.state_dict(), iter_num=self.iter_num)

@@ -53,31 +53,45 @@ class ParamSlot:
     decay: bool
 
 
+def arena_order(model: nn.Module):
+    """(name, parameter) pairs in arena order -- trainable, deduplicated, reverse registration
+    order -- and the number of uses of each parameter (id -> count; > 1 for tied weights)."""
+    uses: dict[int, int] = {}
+    for _, p in model.named_parameters(remove_duplicate=False):
+        uses[id(p)] = uses.get(id(p), 0) + 1
+    seen = set()
+    named = []
+    for name, p in model.named_parameters():
+        if not p.requires_grad or id(p) in seen:
+            continue
+        seen.add(id(p))
+        named.append((name, p))
+    named.reverse()
+    return named, uses
+
+
 class FlatArena:
-    """Owns the flat param/grad buffers of ``model``; rebinds ``p.data``/``p.grad``."""
+    """Owns the flat param/grad buffers of ``model``; rebinds ``p.data``/``p.grad``.
+
+    ``pad_after`` / ``pad_to``: after each named parameter the next offset is rounded up to a
+    multiple of ``pad_to`` elements (ZeRO-1: every data-parallel bucket then splits into
+    ``world`` equal, ALIGN-aligned shards; ``parallel/ddp.py``)."""
 
     SKIP_ZERO_MIN = 1 << 16  # elements: sink slices at least this large are not pre-zeroed
 
     def __init__(self, model: nn.Module, dtype=torch.bfloat16, grad_dtype=None,
-                 device=None, decay_filter=None):
+                 device=None, decay_filter=None, pad_after=(), pad_to: int = ALIGN):
         device = device or next(model.parameters()).device
         grad_dtype = grad_dtype or dtype
         decay_filter = decay_filter or (lambda name, p: p.dim() >= 2)
-        uses: dict[int, int] = {}
-        for _, p in model.named_parameters(remove_duplicate=False):
-            uses[id(p)] = uses.get(id(p), 0) + 1
-        seen = set()
-        named = []
-        for name, p in model.named_parameters():
-            if not p.requires_grad or id(p) in seen:
-                continue
-            seen.add(id(p))
-            named.append((name, p))
-        named.reverse()
+        named, uses = arena_order(model)
+        pad_after = set(pad_after)
+        if pad_to % ALIGN:
+            raise ValueError(f"pad_to must be a multiple of {ALIGN}")
         slots, off = [], 0
         for name, p in named:
             slots.append(ParamSlot(name, p, off, p.numel(), bool(decay_filter(name, p))))
-            off = _round_up(off + p.numel(), ALIGN)
+            off = _round_up(off + p.numel(), pad_to if name in pad_after else ALIGN)
         self.numel = off
         self.slots = slots
         # parameters used by more than one module (GPT-2's wte / LM head): their gradient is

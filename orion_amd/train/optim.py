@@ -43,6 +43,9 @@ class FlatAdamW:
         self._hyper = torch.zeros(8, dtype=torch.float32, device=dev)
         self._use_hip = dev.type == "cuda"
         self._decay_mask = None
+        # ZeRO-1: the squared gradient norm of this rank's shard is summed over the ranks
+        # (in place, on the device) before it sets the clip coefficient
+        self.sumsq_hook = None
 
     # ------------------------------------------------------------------ helpers
     def _decay_mask_full(self):
@@ -72,6 +75,8 @@ class FlatAdamW:
                 self.hyper_tensor()
             ops = C()
             ops.grad_sumsq(a.grads, self._sumsq)
+            if self.sumsq_hook is not None:
+                self.sumsq_hook(self._sumsq)
             ops.adamw_flat(a.params, self.master, self.exp_avg, self.exp_avg_sq, a.grads,
                            a.decay_flags, self._hyper, self._sumsq)
         else:
@@ -81,9 +86,13 @@ class FlatAdamW:
     def _step_reference(self):
         a = self.arena
         g = a.grads.float()
+        sumsq = (g * g).sum().reshape(1)
+        if self.sumsq_hook is not None:
+            self.sumsq_hook(sumsq)
+        self._sumsq.copy_(sumsq)
         if self.grad_clip:
-            norm = g.norm()
-            g = g * min(1.0, self.grad_clip / (float(norm) + 1e-6))
+            norm = float(sumsq.sqrt())
+            g = g * min(1.0, self.grad_clip / (norm + 1e-6))
         b1, b2 = self.betas
         t = self.step_count + 1
         decay = self._decay_mask_full()
@@ -96,7 +105,7 @@ class FlatAdamW:
 
     def grad_norm(self):
         """Global L2 gradient norm of the last step (syncs)."""
-        return math.sqrt(float(self._sumsq)) if self._use_hip else float(self.arena.grads.float().norm())
+        return math.sqrt(float(self._sumsq))
 
     def state_dict(self):
         return dict(step=self.step_count, lr=self.lr, betas=self.betas, eps=self.eps,

@@ -153,8 +153,10 @@ def test_collectives_launch_in_bucket_order():
         dist.destroy_process_group()
 
 
-def test_bench_spawns_its_own_ranks_on_cpu():
-    """``python bench.py --gpus 2`` with no launcher around it starts both ranks itself."""
+@pytest.mark.parametrize("zero1", [False, True])
+def test_bench_spawns_its_own_ranks_on_cpu(zero1):
+    """``python bench.py --gpus 2`` with no launcher around it starts both ranks itself (also
+    with the ZeRO-1 optimizer: half the optimizer state per rank)."""
     import json
     import subprocess
     import sys
@@ -163,7 +165,8 @@ def test_bench_spawns_its_own_ranks_on_cpu():
            ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--model", "gpt2-tiny",
                           "--device", "cpu", "--dist-backend", "gloo", "--seq-len", "64",
-                          "--micro-batch", "2", "--steps", "2", "--warmup", "1"],
+                          "--micro-batch", "2", "--steps", "2", "--warmup", "1"]
+                         + (["--zero1"] if zero1 else []),
                          cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
@@ -177,6 +180,7 @@ def test_bench_spawns_its_own_ranks_on_cpu():
     ddp = rec["ddp_buckets"]
     assert ddp is not None and ddp["exposed_tail_ms"] >= 0
     assert all(done >= ready for _, _, ready, done in ddp["buckets"])
+    assert rec["zero1"] == zero1
 
 
 def test_default_bucket_size_by_model_size():

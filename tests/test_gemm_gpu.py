@@ -125,6 +125,36 @@ def test_fused_mlp_tail_matches_two_node_path(fuse_out_bias, monkeypatch):
         assert rel_err(x, y) < 1e-2, (name, rel_err(x, y))
 
 
+@pytest.mark.parametrize("proj_bias", [False, True])
+@pytest.mark.parametrize("fc_bias", [True, False])
+def test_fused_mlp_matches_reference(proj_bias, fc_bias, monkeypatch):
+    """ops.mlp on the GPU path with ORION_FUSED_MLP (bias + GELU in the fc GEMM's epilogue,
+    GELU' + fc-bias column sums in the projection's input-gradient GEMM) against fp32 autograd
+    of linear -> GELU-tanh -> linear: output and every gradient, ragged token count."""
+    from orion_amd import ops
+    from orion_amd.ops import activations
+    monkeypatch.setattr(activations, "_FUSED_MLP", True)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = _rnd(g, 3, 333, 256)
+    wfc, bfc = _rnd(g, 1024, 256) * 0.1, _rnd(g, 1024)
+    wp, bp = _rnd(g, 256, 1024) * 0.05, _rnd(g, 256)
+    dy = _rnd(g, 3, 333, 256)
+    ts = [t.clone().requires_grad_() for t in (x, wfc, bfc, wp, bp)]
+    y = ops.mlp(ts[0], ts[1], ts[2] if fc_bias else None, ts[3], ts[4] if proj_bias else None)
+    y.backward(dy)
+    fs = [t.detach().float().requires_grad_() for t in (x, wfc, bfc, wp, bp)]
+    a = fs[0] @ fs[1].t() + (fs[2] if fc_bias else 0)
+    yr = ref.gelu_tanh(a) @ fs[3].t() + (fs[4] if proj_bias else 0)
+    yr.backward(dy.float())
+    assert rel_err(y, yr) < 1e-2
+    names = ["dx", "dwfc", "dbfc", "dwproj", "dbproj"]
+    for i, (n, t, f) in enumerate(zip(names, ts, fs)):
+        if (i == 2 and not fc_bias) or (i == 4 and not proj_bias):
+            assert t.grad is None
+            continue
+        assert rel_err(t.grad, f.grad) < 2e-2, (n, rel_err(t.grad, f.grad))
+
+
 def test_gemm_batched_input_shape_and_strided_rows():
     g = torch.Generator(device=DEV).manual_seed(3)
     x = _rnd(g, 4, 96, 256)
@@ -167,3 +197,24 @@ def test_wgrad_phased_and_two_stage_into_fp32(M, N1, N2, cfg, acc, monkeypatch):
     _C().wgrad_into(dy, x, None, out, acc, 0)
     want = dy.float().t() @ x.float() + (base if acc else 0)
     assert rel_err(out, want) < 1e-4
+
+
+@pytest.mark.parametrize("wkm", [False, True])
+def test_gemm16_operands_past_4gb(wkm, monkeypatch):
+    """csrc/gemm16.hip bases its buffer resources at the work item's tile, so a > 4 GB
+    operand (the LM head's logits: 65,536 x 50,304 bf16 = 6.6 GB) stays on the kernel: the
+    forward writes a 4.4 GB output, the input gradient reads a 4.4 GB operand.  Rows at both
+    ends checked against fp32."""
+    monkeypatch.setenv("ORION_GEMM_CFG", "9")
+    g = torch.Generator(device=DEV).manual_seed(7)
+    M, V = 43776, 50304
+    if not wkm:  # out (M, V) = x (M, 64) W (V, 64)^T
+        x, w = _rnd(g, M, 64), _rnd(g, V, 64)
+        out, _ = _C().gemm(x, w, False, 0, None, None)
+        for rows in (slice(0, 256), slice(M - 300, M)):
+            assert rel_err(out[rows], x[rows].float() @ w.float().t()) < 1e-2
+    else:  # out (M, 128) = dl (M, V) W (V, 128)
+        dl, w = _rnd(g, M, V), _rnd(g, V, 128)
+        out, _ = _C().gemm(dl, w, True, 0, None, None)
+        for rows in (slice(0, 256), slice(M - 300, M)):
+            assert rel_err(out[rows], dl[rows].float() @ w.float()) < 1e-2

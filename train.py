@@ -41,6 +41,9 @@ DEFAULTS = dict(
     learning_rate=6e-4, max_iters=600000, weight_decay=1e-1, beta1=0.9, beta2=0.95,
     grad_clip=1.0, decay_lr=True, warmup_iters=2000, lr_decay_iters=600000, min_lr=6e-5,
     backend="nccl", device="cuda", dtype="bfloat16", seed=1337, bucket_mb=0.0,
+    # zero1: shard the fp32 master / Adam state over the data-parallel ranks (ZeRO-1:
+    # reduce-scatter gradients, all-gather weights; parallel/ddp.py ShardedGradReducer)
+    zero1=False,
     data_root="data",
     # tracing: profile_steps > 0 records that many steps, starting at
     # profile_start, with torch.profiler and writes a Chrome trace to out_dir
@@ -138,7 +141,8 @@ def main(argv=None):
                        beta1=cfg["beta1"], beta2=cfg["beta2"], grad_clip=cfg["grad_clip"],
                        warmup_iters=cfg["warmup_iters"], lr_decay_iters=cfg["lr_decay_iters"],
                        min_lr=cfg["min_lr"], decay_lr=cfg["decay_lr"])
-    trainer = Trainer(model, ocfg, ddp=ddp and world > 1, bucket_mb=cfg["bucket_mb"])
+    trainer = Trainer(model, ocfg, ddp=ddp and world > 1, bucket_mb=cfg["bucket_mb"],
+                      zero1=bool(cfg["zero1"]) and ddp)
     best_val = 1e9
     if ckpt is not None:
         restore_trainer(trainer, ckpt)
@@ -195,8 +199,10 @@ def main(argv=None):
                 print(f"step {it}: train loss {last_losses['train']:.4f}, val loss {last_losses['val']:.4f}")
             if last_losses["val"] < best_val or cfg["always_save_checkpoint"]:
                 best_val = min(best_val, last_losses["val"])
-                if it > 0 and master:
-                    save_checkpoint(os.path.join(cfg["out_dir"], "ckpt.pt"), trainer, best_val, cfg)
+                # under ZeRO-1 every rank takes part in gathering the sharded state
+                if it > 0 and (master or trainer.zero1):
+                    save_checkpoint(os.path.join(cfg["out_dir"], "ckpt.pt"), trainer, best_val, cfg,
+                                    write=master)
             if cfg["eval_only"] or it >= cfg["max_iters"]:
                 break
         batches = [train_src.next() for _ in range(A)]
