@@ -56,13 +56,14 @@ def swiglu_hip(gate_up):
     return _SwiGLU.apply(gate_up)
 
 
-# ORION_FUSED_MLP=1 routes the GPT-2 MLP tail through _GeluLinear below.  Off by default: on
-# MI355X the fused backward GEMM (65536 x 3072 x 768) runs 0.62 ms against 0.59 ms for hipBLASLt's
-# dgrad plus the bias_gelu_bwd pass, and the whole GPT-2 step measured 978k vs 990k tok/s (3
-# alternating runs each).  The phased kernel's epilogue runs after its MMAs on the same waves
-# (one 160 KB-LDS workgroup per CU), so the (M, F) pre-activation read is not overlapped with
-# matrix work: +205 us over the plain-store kernel (profiles/gemm_study/epilogue_cost.txt).
-_FUSED_MLP = os.environ.get("ORION_FUSED_MLP", "0") != "0"
+# ORION_FUSED_MLP (default on since round 3): the GPT-2 MLP as GEMMs with fused epilogues
+# (_FusedMLP below; also routes gelu_linear through _GeluLinear).  On the 16x16x32-MFMA kernel
+# (csrc/gemm16.hip) the fused forward runs 0.41 ms per layer in the step against 0.39 for
+# hipBLASLt + the bias_gelu pass, the fused backward 0.48 against 0.48 -- a wash per layer,
+# but with the in-tree input gradients the whole step gains 0.4 % (three alternating runs,
+# profiles/ab/ab_gemm_auto_fusedmlp_r03e.log) and two (M, 4C) HBM passes per layer are gone.
+# Round 2's 32x32x16 kernel lost (978k vs 990k tok/s): its fused epilogue cost more.
+_FUSED_MLP = os.environ.get("ORION_FUSED_MLP", "1") != "0"
 
 
 def fused_mlp_ok(a, weight) -> bool:

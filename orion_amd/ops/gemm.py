@@ -29,14 +29,17 @@ from ._ext import C
 from .determinism import deterministic
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
-# Linear-layer forward (x W^T [+ b]) and input gradient (dy W).  ORION_GEMM=blas: hipBLASLt.
-# ORION_GEMM=auto: every input gradient on the in-tree 16x16x32-MFMA kernel (csrc/gemm16.hip:
-# the GPT-2 qkv / attn-proj / fc dgrads run 8-25 % faster than hipBLASLt in isolation,
-# profiles/gemm16/), forward GEMMs on hipBLASLt.  ORION_GEMM=hip routes every eligible GEMM
-# in-tree.  Inside a HIP-graph capture (``hip_gemms()``)
+# Linear-layer forward (x W^T [+ b]) and input gradient (dy W).  ORION_GEMM=auto (default):
+# every input gradient on the in-tree 16x16x32-MFMA kernel (csrc/gemm16.hip: the GPT-2 qkv /
+# attn-proj / fc / LM-head dgrads run 4-25 % faster than hipBLASLt in isolation,
+# profiles/gemm16/), plain forward GEMMs on hipBLASLt (the in-tree kernel loses 1-10 % there
+# and 45 % on the K = 768 LM head).  ORION_GEMM=blas: hipBLASLt for all; ORION_GEMM=hip: every
+# eligible GEMM in-tree.  Whole GPT-2 step, same box, 3 alternating runs
+# (profiles/ab/ab_gemm_auto_fusedmlp_r03e.log): blas 1,047.7-1,048.8k, auto 1,045.6-1,048.8k,
+# auto + fused MLP (ops/activations.py) 1,048.5-1,054.9k, hip + fused MLP 1,009.4-1,012.3k tok/s.  Inside a HIP-graph capture (``hip_gemms()``)
 # every eligible GEMM is in-tree (no library-side host state between replays), and so in the
 # deterministic mode (ops/determinism.py): one workgroup per output tile, no split-K.
-_GEMM_IMPL = os.environ.get("ORION_GEMM", "blas")  # "blas" | "auto" | "hip"
+_GEMM_IMPL = os.environ.get("ORION_GEMM", "auto")  # "auto" | "blas" | "hip"
 _FORCE_HIP = 0
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD = 0, 1, 2, 3
