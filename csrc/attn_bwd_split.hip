@@ -69,7 +69,11 @@ ORION_DEVICE bf16x8 bwd_buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsi
 template <int D>
 __host__ __device__ constexpr int kv_waves() { return 4; }
 
-template <int D, bool CAUSAL>
+// STAMPS (diagnostic instantiation, ORION_ATTN_DIAG=1, D = 64): every wave accumulates
+// s_memtime deltas of the five phases of a query tile (S/dP chain issue, softmax, dV/dK
+// issue, LDS stage write, barrier) and writes them with its active-tile count and lifetime
+// over p.dq (the dQ kernel is then skipped): scripts/attn_stamps.py, profiles/attn_r03/.
+template <int D, bool CAUSAL, bool STAMPS = false>
 __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
   constexpr int NW = kv_waves<D>(), NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
@@ -215,8 +219,22 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
     swrite(0);
   }
   __syncthreads();
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_prev = 0, st_begin = 0;
+  int st_n = 0;
+  auto stamp = [&](int k) {
+    if constexpr (STAMPS) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (k >= 0) st_acc[k] += t - st_prev;
+      st_prev = t;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp(-1);
+  st_begin = st_prev;
   int cq = qi0;  // query tile of this step
   for (int it = 0; it < total; ++it) {
+    stamp(-1);
     const int buf = it & 1;
     const int qbase = cq * BMQ;
     if (++cq == nqi) cq = qi0;
@@ -248,6 +266,8 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
         dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
         if constexpr (KLDS) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
       }
+      stamp(0);
+      ++st_n;
       // P and dS in place: row q = qbase + (r&3)+8(r>>2)+4*h32, column = mykey
       const bool need_mask = (CAUSAL && (qbase + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
                              (qbase + BMQ > p.T);
@@ -273,6 +293,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
       pb[1] = acc_to_frag(s, 1);
       sb[0] = acc_to_frag(dp, 0);
       sb[1] = acc_to_frag(dp, 1);
+      stamp(1);
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
 #pragma unroll
@@ -281,9 +302,22 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
           dka[db] = mfma32(tr_frag<D>(Qc, 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
         }
       }
+      stamp(2);
     }
     if (it + 1 < total) swrite(buf ^ 1);
+    stamp(3);
     __syncthreads();
+    stamp(4);
+  }
+  if constexpr (STAMPS) {
+    if (lane == 0) {
+      unsigned long long* out = reinterpret_cast<unsigned long long*>(p.dq) + ((long)blockIdx.x * NW + wv) * 8;
+      for (int k = 0; k < 5; ++k) out[k] = st_acc[k];
+      out[5] = (unsigned long long)st_n;
+      out[6] = (unsigned long long)total;
+      out[7] = st_prev - st_begin;
+    }
+    return;
   }
 
   // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
@@ -528,8 +562,13 @@ static bool delta_fused() {
 // outputs (strided views allowed).  Default order: delta pass, dK/dV, dQ; with
 // ORION_ATTN_DELTA=fused: dQ (computing and writing delta), then dK/dV (reading it).
 int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
-  // the dQ kernel addresses one (batch, KV head)'s K / V with 32-bit buffer offsets
-  if (((long)(p.Tk - 1) * p.k_st + D) * 2 >= (1L << 31) || ((long)(p.Tk - 1) * p.v_st + D) * 2 >= (1L << 31))
+  // 32-bit buffer offsets: the dQ kernel addresses one (batch, KV head)'s K / V, the dK/dV
+  // kernel one batch's Q / dO over all query heads; beyond 2 GB the caller takes the fused
+  // form (64-bit addressing)
+  constexpr long LIM = 1L << 31;
+  if (((long)(p.Tk - 1) * p.k_st + D) * 2 >= LIM || ((long)(p.Tk - 1) * p.v_st + D) * 2 >= LIM ||
+      ((long)(p.T - 1) * p.q_st + (long)(p.Hq - 1) * p.q_sh + D) * 2 >= LIM ||
+      ((long)(p.T - 1) * p.do_st + (long)(p.Hq - 1) * p.do_sh + D) * 2 >= LIM)
     return -2;
   const long rows = (long)p.B * p.Hq * p.T;
   const int pre_grid = (int)((rows * (D / 8) + 255) / 256);
@@ -538,6 +577,20 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   const int kv_grid = ((p.Tk + 32 * 4 - 1) / (32 * 4)) * p.B * p.Hkv;
   const int dq_grid = ((p.T + 127) / 128) * p.B * p.Hq;
   const bool fused = delta_fused();
+  static const bool diag = getenv("ORION_ATTN_DIAG") && getenv("ORION_ATTN_DIAG")[0] == '1';
+  if (diag && D == 64) {  // stamped dK/dV kernel only, stamps over p.dq (scripts/attn_stamps.py)
+    attn_delta_kernel<64><<<pre_grid, 256, 0, st>>>(p, delta);
+    if (causal) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<64, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(64));
+      attn_bwd_kv_kernel<64, true, true><<<kv_grid, kv_waves<64>() * 64, kv_lds(64), st>>>(q);
+    } else {
+      (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<64, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(64));
+      attn_bwd_kv_kernel<64, false, true><<<kv_grid, kv_waves<64>() * 64, kv_lds(64), st>>>(q);
+    }
+    return (int)hipGetLastError();
+  }
 #define SPLIT(DD, CC)                                                                   \
   split_attrs<DD, CC>();                                                                \
   if (fused) {                                                                          \

@@ -784,9 +784,11 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   if (attn_bwd_use_split(D, flags)) {
     p.dq = (unsigned short*)dq.data_ptr();
     p.dq_sb = dq.stride(0); p.dq_st = dq.stride(1); p.dq_sh = dq.stride(2);
-    check_launch(orion_attn_bwd_split(p, D, causal, delta.data_ptr<float>(), cur_stream()),
-                 "attn_bwd_split");
-    return;
+    const int rc = orion_attn_bwd_split(p, D, causal, delta.data_ptr<float>(), cur_stream());
+    if (rc != -2) {  // -2: operands beyond the split kernels' 32-bit offsets -> fused form
+      check_launch(rc, "attn_bwd_split");
+      return;
+    }
   }
   auto dq_acc = at::empty({p.B, p.Hq, p.T, D}, fopts);
   p.dq_acc = dq_acc.data_ptr<float>();

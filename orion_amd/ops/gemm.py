@@ -36,13 +36,21 @@ from .determinism import deterministic
 # and 45 % on the K = 768 LM head).  ORION_GEMM=blas: hipBLASLt for all; ORION_GEMM=hip: every
 # eligible GEMM in-tree.  Whole GPT-2 step, same box, 3 alternating runs
 # (profiles/ab/ab_gemm_auto_fusedmlp_r03e.log): blas 1,047.7-1,048.8k, auto 1,045.6-1,048.8k,
-# auto + fused MLP (ops/activations.py) 1,048.5-1,054.9k, hip + fused MLP 1,009.4-1,012.3k tok/s.  Inside a HIP-graph capture (``hip_gemms()``)
-# every eligible GEMM is in-tree (no library-side host state between replays), and so in the
-# deterministic mode (ops/determinism.py): one workgroup per output tile, no split-K.
+# auto + fused MLP (ops/activations.py) 1,048.5-1,054.9k, hip + fused MLP 1,009.4-1,012.3k
+# tok/s.  Inside a HIP-graph capture (``hip_gemms()``) every eligible GEMM is in-tree (no
+# library-side host state between replays), and so in the deterministic mode
+# (ops/determinism.py): one workgroup per output tile, no split-K.
 _GEMM_IMPL = os.environ.get("ORION_GEMM", "auto")  # "auto" | "blas" | "hip"
 _FORCE_HIP = 0
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD = 0, 1, 2, 3
+
+
+# GEMMs that fell back to a library call inside ``hip_gemms()`` (ineligible shape, stride or
+# alignment): (kind, shape) records.  A captured HIP graph must not contain library GEMMs
+# (round 1: captured hipBLASLt GEMMs faulted on replay at 65k tokens), so the trainer checks
+# this after its warm-up steps and stays eager, with a warning, when anything fell back.
+_FORCED_FALLBACKS: list = []
 
 
 @contextlib.contextmanager
@@ -54,6 +62,19 @@ def hip_gemms():
         yield
     finally:
         _FORCE_HIP -= 1
+
+
+def forced_fallbacks(clear: bool = False) -> list:
+    """The library fallbacks recorded inside ``hip_gemms()`` so far (see above)."""
+    out = list(_FORCED_FALLBACKS)
+    if clear:
+        _FORCED_FALLBACKS.clear()
+    return out
+
+
+def _note_fallback(kind: str, *tensors):
+    if _FORCE_HIP and len(_FORCED_FALLBACKS) < 64:
+        _FORCED_FALLBACKS.append((kind, tuple(tuple(t.shape) for t in tensors)))
 
 
 def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
@@ -82,6 +103,7 @@ def linear_fwd(x, w, b=None):
     """x W^T (+ b): csrc/gemm.hip when selected (see above), else hipBLASLt."""
     if use_hip_gemm(x, w, False):
         return C().gemm(x, w, False, EPI_BIAS if b is not None else EPI_STORE, b, None)[0]
+    _note_fallback("linear_fwd", x, w)
     return torch.nn.functional.linear(x, w, b)
 
 
@@ -89,6 +111,7 @@ def linear_dgrad(dy, w):
     """dy W for W (N_out, N_in): the input gradient of x W^T."""
     if use_hip_gemm(dy, w, True):
         return C().gemm(dy, w, True, EPI_STORE, None, None)[0]
+    _note_fallback("linear_dgrad", dy, w)
     return dy @ w
 
 # Order of a linear layer's two backward GEMMs.  Both read dY; the input gradient dX is
@@ -129,7 +152,7 @@ def _blas_wins(n1: int, n2: int) -> bool:
     Llama-7B shapes at 16k tokens (12288/4096/22016/32000 x 4096 and 4096 x 11008: 9.8 vs
     10.75 ms in total, profiles/gemm_study/bench_wgrad_llama_shapes.log), where csrc/wgrad.hip
     used to lose by 5-12 %."""
-    return _IMPL == "blas" and not deterministic()
+    return _IMPL == "blas" and not deterministic() and not _FORCE_HIP
 
 
 def wgrad_into(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool,
@@ -151,6 +174,7 @@ def wgrad_into(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate:
     elif _hip_ok(dy, x):
         C().wgrad_into(dy, x, scale, out.view(n1, n2), bool(accumulate), int(_FORCE or 0))
     else:
+        _note_fallback("wgrad_into", dy, x)
         g = wgrad(dy, x, scale)
         if accumulate:
             out.view(n1, n2).add_(g)
@@ -164,6 +188,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, scale: torch.Tensor | None = None) 
         return dy.t() @ x
     if _hip_ok(dy, x):
         return C().wgrad(dy, x, scale, int(_FORCE or 0))
+    _note_fallback("wgrad", dy, x)
     M, n1 = dy.shape
     n2 = x.shape[1]
     S = wgrad_splits(M, n1, n2)

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
-from ..ops.gemm import hip_gemms
+from ..ops.gemm import forced_fallbacks, hip_gemms
 from .flat import FlatArena
 from .optim import FlatAdamW
 
@@ -175,11 +175,18 @@ class Trainer:
             if self._side is None:
                 self._side = torch.cuda.Stream()
             self._side.wait_stream(torch.cuda.current_stream())
+            forced_fallbacks(clear=True)
             with torch.cuda.stream(self._side), hip_gemms():
                 self.opt.hyper_tensor()
                 loss = self._body(batches)
             torch.cuda.current_stream().wait_stream(self._side)
             self.iter_num += 1
+            fb = forced_fallbacks(clear=True)
+            if fb:
+                # a library GEMM must not be captured (ops/gemm.py _FORCED_FALLBACKS): eager
+                print(f"[orion_amd] HIP-graph capture disabled: {len(fb)} GEMM(s) not eligible for "
+                      f"the in-tree kernels, e.g. {fb[0]}; the step runs eagerly", flush=True)
+                self.graph_enabled = False
             return loss
         if self._graph is None:
             self._static = [(x.clone(), y.clone()) for x, y in batches]

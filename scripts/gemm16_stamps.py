@@ -8,7 +8,6 @@ issue, barrier wait out of it; plus prologue, main loop, epilogue and the k-tile
 usage: python scripts/gemm16_stamps.py M N K wkm"""
 import json
 import os
-import statistics as stt
 import sys
 
 import torch

@@ -135,3 +135,21 @@ def test_embed_layer_norm_cpu_path_matches_unfused():
     for a, t in zip(g, (wte, wpe, w, b)):
         assert torch.allclose(a, t.grad, atol=1e-4)
     assert float(g[1][T:].abs().max()) == 0.0
+
+
+def test_gemms_forced_in_tree_record_library_fallbacks():
+    """Inside ``hip_gemms()`` (HIP-graph capture) a GEMM that is not eligible for the in-tree
+    kernels falls back to a library call; that fallback is recorded so the trainer can keep the
+    step eager instead of capturing a library GEMM (ops/gemm.py)."""
+    from orion_amd.ops import gemm
+    gemm.forced_fallbacks(clear=True)
+    x, w = torch.randn(4, 8), torch.randn(6, 8)
+    gemm.linear_fwd(x, w)  # outside the block: nothing recorded
+    assert gemm.forced_fallbacks() == []
+    with gemm.hip_gemms():
+        y = gemm.linear_fwd(x, w)
+        gemm.linear_dgrad(torch.randn(4, 6), w)
+    assert torch.allclose(y, x @ w.t())
+    fb = gemm.forced_fallbacks(clear=True)
+    assert [k for k, _ in fb] == ["linear_fwd", "linear_dgrad"] and fb[0][1] == ((4, 8), (6, 8))
+    assert gemm.forced_fallbacks() == []
