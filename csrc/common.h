@@ -46,8 +46,15 @@ ORION_DEVICE bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_v;
+
+// two floats -> one word of two bf16 (RNE) in ONE v_cvt_pk_bf16_f32; the OR of two scalar
+// casts compiled to a cvt per value plus an and / shift / v_or_b32_sdwa repack
 ORION_DEVICE unsigned pack_bf16x2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{lo, hi}), bf16x2_v));
+}
+ORION_DEVICE unsigned pack2_bf16(f32x2 v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_v));
 }
 
 // Gradient-arena element I/O: the arena is fp32 by default (accumulation over micro-batches
@@ -110,28 +117,39 @@ ORION_DEVICE float block_max(float v, float* scratch) {
 }
 
 // GELU (tanh approximation) and its derivative, as in GPT-2 / nanoGPT.
-// 0.5 (1 + tanh(u)) == sigmoid(2u) = 1 / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32
-// instead of a tanhf expansion (the activation kernels are HBM-bound only if the VALU keeps up).
-ORION_DEVICE float sigmoid2u_(float x, float* x2out) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float m2log2e = -2.8853900817779268f;  // -2 * log2(e)
-  const float x2 = x * x;
-  *x2out = x2;
-  const float u = k0 * fmaf(k1 * x2, x, x);
-  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * m2log2e));
-}
+// 0.5 (1 + tanh(u)) == sigmoid(2u) = 1 / (1 + 2^z): one v_exp_f32 + one v_rcp_f32 instead of
+// a tanhf expansion, with u = k0 (x + k1 x^3) and every constant folded into
+// z = x (GELU_A + GELU_B x^2): GELU_A = -2 log2(e) k0, GELU_B = GELU_A k1 (k0 = sqrt(2/pi),
+// k1 = 0.044715).  d/dx [x s] = s + s (1 - s) x (GELU_C + GELU_D x^2), GELU_C = 2 k0,
+// GELU_D = 6 k0 k1.
+constexpr float GELU_A = -2.302208198144325f, GELU_B = -0.1029432395800235f;
+constexpr float GELU_C = 1.5957691216057308f, GELU_D = 0.21406444881780076f;
 
 ORION_DEVICE float gelu_tanh_f(float x) {
-  float x2;
-  return x * sigmoid2u_(x, &x2);
+  const float z = x * fmaf(x * x, GELU_B, GELU_A);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
 }
 
 ORION_DEVICE float gelu_tanh_grad_f(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2;
-  const float s = sigmoid2u_(x, &x2);
-  // d/dx [x s(2u)] = s + x * 2 s (1 - s) * u'(x),  u' = k0 (1 + 3 k1 x^2)
-  return fmaf(x * 2.f * s * (1.f - s), k0 * fmaf(3.f * k1, x2, 1.f), s);
+  const float x2 = x * x;
+  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * fmaf(x2, GELU_B, GELU_A)));
+  return fmaf(fmaf(-s, s, s), x * fmaf(x2, GELU_D, GELU_C), s);
+}
+
+// Two values per instruction (v_pk_mul / v_pk_fma / v_pk_add_f32) for the GEMM epilogues,
+// where no MFMA runs beside the VALU (beside MFMAs packed f32 ops cost more than two single
+// ones: MI355X_MICROARCH.md); the exp2 / rcp stay one per value.
+ORION_DEVICE f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+ORION_DEVICE f32x2 splat2(float v) { return f32x2{v, v}; }
+ORION_DEVICE f32x2 sigmoid2u_x2(f32x2 x, f32x2 x2) {
+  const f32x2 z = x * fma2(x2, splat2(GELU_B), splat2(GELU_A));
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + splat2(1.f);
+  return f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+ORION_DEVICE f32x2 gelu_x2(f32x2 x) { return x * sigmoid2u_x2(x, x * x); }
+ORION_DEVICE f32x2 gelu_grad_x2(f32x2 x) {
+  const f32x2 x2 = x * x, s = sigmoid2u_x2(x, x2);
+  return fma2(fma2(-s, s, s), x * fma2(x2, splat2(GELU_D), splat2(GELU_C)), s);
 }
 
 ORION_DEVICE float silu_f(float x) { return x / (1.f + __expf(-x)); }

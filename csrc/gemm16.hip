@@ -380,70 +380,76 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   if constexpr (EPI == EPI_BIAS_GELU)
     ro2 = make_rsrc(g.out2 + (long)m0 * g.ldo2, (unsigned)(((long)(rows_m - 1) * g.ldo2 + g.N) * 2));
   constexpr bool CS = EPI == EPI_GELU_BWD;
+  // bf16 pair word -> two floats (low half first)
+  auto unpack2 = [](unsigned w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)}; };
+  // the value arithmetic runs on pairs of adjacent columns (v_pk_*_f32: no MFMA issues beside
+  // the epilogue) and every pair is packed to bf16 by one v_cvt_pk_bf16_f32
 #pragma unroll
   for (int ap = 0; ap < 4; ++ap) {
     // after the swap: lane (q, i16) holds n = nb .. nb + 7 of row m (fp32)
     const int nb = nw + 16 * (2 * ap + (q & 1)) + 8 * (q >> 1);
     const bool nok = nb < g.N;
     const int nc = nok ? nb : 0;
-    [[maybe_unused]] float bias[8];
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
-      const bf16x8 b8 = *reinterpret_cast<const bf16x8*>(g.bias + nc);
+    [[maybe_unused]] f32x2 bias[4];
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_GELU_BWD) {
+      if (EPI != EPI_GELU_BWD || g.bias) {
+        const u32x4 b4 = *reinterpret_cast<const u32x4*>(g.bias + nc);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) bias[e] = bf2f(b8[e]);
-    }
-    if constexpr (EPI == EPI_GELU_BWD) {
-      if (g.bias) {
-        const bf16x8 b8 = *reinterpret_cast<const bf16x8*>(g.bias + nc);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bias[e] = bf2f(b8[e]);
+        for (int e = 0; e < 4; ++e) bias[e] = unpack2(b4[e]);
       } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+        for (int e = 0; e < 4; ++e) bias[e] = splat2(0.f);
       }
     }
-    [[maybe_unused]] float cs[8];
+    [[maybe_unused]] f32x2 cs[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int m = mw + 16 * b + i16;
       const int mc = min(m, g.M - 1);
-      float v[8];
+      [[maybe_unused]] u32x4 p4;
+      if constexpr (EPI == EPI_GELU_BWD) p4 = *reinterpret_cast<const u32x4*>(g.pre + (long)mc * g.ldp + nc);
+      f32x2 v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * ap][b][r]),
                                                          __float_as_uint(acc[2 * ap + 1][b][r]), false, false);
-        v[r] = __uint_as_float(sw[0]);
-        v[4 + r] = __uint_as_float(sw[1]);
+        v[r >> 1][r & 1] = __uint_as_float(sw[0]);
+        v[2 + (r >> 1)][r & 1] = __uint_as_float(sw[1]);
       }
       if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bias[e];
+        for (int e = 0; e < 4; ++e) v[e] += bias[e];
       }
       if constexpr (EPI == EPI_GELU_BWD) {
-        const bf16x8 p8 = *reinterpret_cast<const bf16x8*>(g.pre + (long)mc * g.ldp + nc);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad_f(bf2f(p8[e]) + bias[e]);
+        for (int e = 0; e < 4; ++e) v[e] *= gelu_grad_x2(unpack2(p4[e]) + bias[e]);
       }
       const bool ok = m < g.M && nok;
       const unsigned off = ok ? (unsigned)(((long)(m - m0) * g.ldo + nb) * 2) : 0xFFFFFFF0u;
       u32x4 pk;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+      for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(v[e]);
       __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, 0);
       if constexpr (EPI == EPI_BIAS_GELU) {
         const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(gelu_tanh_f(v[2 * e]), gelu_tanh_f(v[2 * e + 1]));
+        for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(gelu_x2(v[e]));
         __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off2, 0, 0);
       }
       if constexpr (CS) {
-        const float keep = m < g.M ? 1.f : 0.f;  // rows past M repeat row M - 1
+        const f32x2 keep = splat2(m < g.M ? 1.f : 0.f);  // rows past M repeat row M - 1
 #pragma unroll
-        for (int e = 0; e < 8; ++e) cs[e] = b ? cs[e] + keep * v[e] : keep * v[e];
+        for (int e = 0; e < 4; ++e) cs[e] = b ? fma2(keep, v[e], cs[e]) : keep * v[e];
       }
     }
     if constexpr (CS) {
       if (g.colsum) {
+        float c8[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          c8[2 * e] = cs[e].x;
+          c8[2 * e + 1] = cs[e].y;
+        }
         // sum over the 16 lanes of each row group (same n, m = i16): three halving exchange
         // steps (at offset o a lane keeps the half of its live values selected by lane bit o
         // and adds its partner's copy of it), then one full add with lane ^ 1; lane i16 ends
@@ -453,15 +459,15 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
           const bool up = (i16 & o) != 0;
 #pragma unroll
           for (int k = 0; k < half; ++k) {
-            const float send = up ? cs[k] : cs[half + k];
-            const float keep = up ? cs[half + k] : cs[k];
-            cs[k] = keep + __shfl_xor(send, o);
+            const float send = up ? c8[k] : c8[half + k];
+            const float keep = up ? c8[half + k] : c8[k];
+            c8[k] = keep + __shfl_xor(send, o);
           }
         };
         step(std::integral_constant<int, 8>());
         step(std::integral_constant<int, 4>());
         step(std::integral_constant<int, 2>());
-        const float tot = cs[0] + __shfl_xor(cs[0], 1);
+        const float tot = c8[0] + __shfl_xor(c8[0], 1);
         const int n = nb + ((i16 >> 1) & 7);
         if (!(i16 & 1) && mw < g.M && n < g.N) g.colsum[(long)(mw / 64) * g.N + n] = tot;
       }
