@@ -59,6 +59,43 @@ ORION_DEVICE bf16x8 bwd_buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsi
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+// Column sums over a wave's 32 rows (lane l32 = row, h32 = d half) of the NDB f32x16
+// accumulators x * sc: d = 32 db + (r & 3) + 8 (r >> 2) + 4 h32.  Five halving exchange steps
+// over the lane bits (at offset o a lane keeps the half of its live values selected by bit o
+// of l32 and adds its partner's copy of it): 31 shuffles for 32 values instead of a
+// butterfly per value.  Lane l32 ends with values l32 * (NV / 32) + j, written to
+// dst[d(value)]; rows past the end contribute 0 (valid = false).
+template <int NDB>
+ORION_DEVICE void wave_colsum_store(const f32x16 (&x)[NDB], float sc, bool valid, int l32, int h32,
+                                    float* __restrict__ dst) {
+  constexpr int NV = 16 * NDB;
+  float v[NV];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[16 * db + r] = valid ? x[db][r] * sc : 0.f;
+  auto step = [&](auto Oc, auto Lc) {
+    constexpr int o = decltype(Oc)::value, L = decltype(Lc)::value, half = L / 2;
+    const bool up = (l32 & o) != 0;
+#pragma unroll
+    for (int k = 0; k < half; ++k) {
+      const float send = up ? v[k] : v[half + k];
+      const float keep = up ? v[half + k] : v[k];
+      v[k] = keep + __shfl_xor(send, o);
+    }
+  };
+  step(std::integral_constant<int, 16>(), std::integral_constant<int, NV>());
+  step(std::integral_constant<int, 8>(), std::integral_constant<int, NV / 2>());
+  step(std::integral_constant<int, 4>(), std::integral_constant<int, NV / 4>());
+  step(std::integral_constant<int, 2>(), std::integral_constant<int, NV / 8>());
+  step(std::integral_constant<int, 1>(), std::integral_constant<int, NV / 16>());
+#pragma unroll
+  for (int j = 0; j < NV / 32; ++j) {
+    const int idx = l32 * (NV / 32) + j, db = idx >> 4, r = idx & 15;
+    dst[32 * db + (r & 3) + 8 * (r >> 2) + 4 * h32] = v[j];
+  }
+}
+
 // ============================================================================ dK / dV
 // NW waves x 32 keys per workgroup; query tiles of 32 rows double-buffered in LDS
 // (register staged: the next tile's loads are issued before this tile's MFMAs and written
@@ -73,8 +110,8 @@ __host__ __device__ constexpr int kv_waves() { return 4; }
 // s_memtime deltas of the five phases of a query tile (S/dP chain issue, softmax, dV/dK
 // issue, LDS stage write, barrier) and writes them with its active-tile count and lifetime
 // over p.dq (the dQ kernel is then skipped): scripts/attn_stamps.py, profiles/attn_r03/.
-template <int D, bool CAUSAL, bool STAMPS = false>
-__global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
+template <int D, bool CAUSAL, bool STAMPS = false, bool BIAS = false>
+__global__ __launch_bounds__(kv_waves<D>() * 64, BIAS ? 3 : 2) void attn_bwd_kv_kernel(AttnParams p) {
   constexpr int NW = kv_waves<D>(), NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
   constexpr int QT = BMQ * D;            // Q / dO tile elements
@@ -321,6 +358,13 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
   }
 
   // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
+  if (BIAS && kw0 < p.Tk) {  // column sums of this wave's 32 keys (packed QKV bias grad)
+    float* row = p.bias_part + ((long)b * ((p.Tk + 31) / 32) + kw0 / 32) * p.bias_ld + (p.Hq + hk) * D;
+    wave_colsum_store<NDB>(dka, p.scale, mykey < p.Tk, l32, h32, row);
+    __builtin_amdgcn_sched_barrier(0);
+    wave_colsum_store<NDB>(dva, 1.f, mykey < p.Tk, l32, h32, row + p.Hkv * D);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   if (mykey < p.Tk) {
     bf16_t* dKb = p.dk + b * p.dk_sb + hk * p.dk_sh + (long)mykey * p.dk_st;
     bf16_t* dVb = p.dv + b * p.dv_sb + hk * p.dv_sh + (long)mykey * p.dv_st;
@@ -350,7 +394,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 // fragments it holds anyway plus the matching half-row of O (one more 16-byte load per
 // k-step, the halves joined by one lane exchange), and writes it for the dK/dV kernel,
 // which is then launched after this one: no separate delta pass over O and dO.
-template <int D, bool CAUSAL, bool FUSE_DELTA>
+template <int D, bool CAUSAL, bool FUSE_DELTA, bool BIAS = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
@@ -505,6 +549,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
     if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
   }
 
+  if (BIAS && qw0 < p.T)  // column sums of this wave's 32 queries (packed QKV bias grad)
+    wave_colsum_store<NDB>(dq, p.scale, myq < p.T, l32, h32,
+                           p.bias_part + ((long)b * ((p.T + 31) / 32) + qw0 / 32) * p.bias_ld + hq * D);
   if (myq < p.T) {
     ORION_DASSERT(b < p.B && hq < p.Hq);
     bf16_t* Qo = p.dq + b * p.dq_sb + hq * p.dq_sh + (long)myq * p.dq_st;
@@ -541,6 +588,18 @@ static void split_attrs() {
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
     hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, true>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
+    done = true;
+  }
+}
+
+template <bool CAUSAL>
+static void bias_attrs() {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<64, CAUSAL, false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(64));
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<64, CAUSAL, false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(64));
     done = true;
   }
 }
@@ -589,6 +648,18 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(64));
       attn_bwd_kv_kernel<64, false, true><<<kv_grid, kv_waves<64>() * 64, kv_lds(64), st>>>(q);
     }
+    return (int)hipGetLastError();
+  }
+  if (p.bias_part) {  // packed self-attention with the QKV bias gradient (GPT-2: D = 64)
+    if (D != 64 || fused || p.T != p.Tk) return -3;
+    q.bias_part = p.bias_part;
+#define SPLITB(CC)                                                                                  \
+  bias_attrs<CC>();                                                                                 \
+  attn_delta_kernel<64><<<pre_grid, 256, 0, st>>>(p, delta);                                        \
+  attn_bwd_kv_kernel<64, CC, false, true><<<kv_grid, kv_waves<64>() * 64, kv_lds(64), st>>>(q);     \
+  attn_bwd_dq_kernel<64, CC, false, true><<<dq_grid, 256, dq_lds(64), st>>>(q);
+    if (causal) { SPLITB(true) } else { SPLITB(false) }
+#undef SPLITB
     return (int)hipGetLastError();
   }
 #define SPLIT(DD, CC)                                                                   \

@@ -744,6 +744,14 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
 // default (MI355X: 0.632 vs 0.722 ms at B64 T1024 H12 D64, 3.39 vs 4.46 ms at B4 T4096
 // H32/8 D128); flags bit 2 (deterministic) forces split, bit 3 forces fused; otherwise
 // ORION_ATTN_BWD = split | v1 | v2 overrides the default.
+// column sums of the packed bf16 dQKV starting at dq ([rows][ld], contiguous)
+void attn_bias_colsum_packed(const Tensor& dq, const Tensor& out, long rows, long ld) {
+  auto part = at::empty({(long)orion_colsum_scratch((int)rows, (int)ld)}, dq.options().dtype(at::kFloat));
+  check_launch(orion_colsum_bf16(dq.data_ptr(), out.data_ptr(), part.data_ptr<float>(), (int)rows, (int)ld,
+                                 is_f32(out), cur_stream()),
+               "attn_bias_colsum");
+}
+
 bool attn_bwd_use_split(int D, int64_t flags) {
   if (flags & 4) return true;
   if (flags & 8) return false;  // force the fused form (A/B tests)
@@ -757,9 +765,13 @@ bool attn_bwd_use_split(int D, int64_t flags) {
 }
 
 // dq/dk/dv: preallocated outputs (may be strided views of one packed buffer)
+// bias_grad (optional): the QKV projection's bias gradient, colsum over tokens of the packed
+// (B, T, Hq + 2 Hkv, D) dQKV that dq / dk / dv must then be views of.  The split kernels sum
+// their fp32 outputs per 32-token block (AttnParams::bias_part) and a two-stage fold writes
+// bias_grad (fp32 arena slice or bf16); other backward forms sum the packed bf16 dQKV.
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
               const Tensor& o, const Tensor& lse, bool causal, double scale, Tensor dq, Tensor dk,
-              Tensor dv, int64_t flags) {
+              Tensor dv, int64_t flags, const c10::optional<Tensor>& bias_grad) {
   check_attn_inputs(q, k, v);
   check_bf16(dout, "dout");
   TORCH_CHECK(dout.stride(3) == 1 && o.stride(3) == 1, "dout/o head dim must be contiguous");
@@ -781,14 +793,45 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   p.dv = (unsigned short*)dv.data_ptr();
   p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
   p.flags = (int)flags;
+  const long ld = (long)(p.Hq + 2 * p.Hkv) * D;
+  const bool want_bias = has_out(bias_grad, ld, "bias_grad");
+  Tensor bpart;
+  if (want_bias) {
+    const long e = dq.element_size();
+    TORCH_CHECK(p.T == p.Tk && dq.stride(1) == ld && dk.stride(1) == ld && dv.stride(1) == ld &&
+                    dq.stride(0) == p.T * ld && dq.stride(2) == D && dk.stride(2) == D &&
+                    dv.stride(2) == D &&
+                    (char*)dk.data_ptr() == (char*)dq.data_ptr() + p.Hq * D * e &&
+                    (char*)dv.data_ptr() == (char*)dk.data_ptr() + p.Hkv * D * e,
+                "bias_grad needs dq / dk / dv to be views of one packed (B, T, Hq + 2 Hkv, D) dQKV");
+  }
   if (attn_bwd_use_split(D, flags)) {
     p.dq = (unsigned short*)dq.data_ptr();
     p.dq_sb = dq.stride(0); p.dq_st = dq.stride(1); p.dq_sh = dq.stride(2);
-    const int rc = orion_attn_bwd_split(p, D, causal, delta.data_ptr<float>(), cur_stream());
+    const long prow = (long)p.B * ((p.T + 31) / 32);
+    if (want_bias && D == 64) {
+      bpart = at::empty({prow * ld + 16 * ld}, fopts);  // partials + the fold's scratch
+      p.bias_part = bpart.data_ptr<float>();
+      p.bias_ld = (int)ld;
+    }
+    int rc = orion_attn_bwd_split(p, D, causal, delta.data_ptr<float>(), cur_stream());
+    if (rc == -3) {  // no in-kernel column sums for this form: plain kernels, summed below
+      p.bias_part = nullptr;
+      rc = orion_attn_bwd_split(p, D, causal, delta.data_ptr<float>(), cur_stream());
+    }
     if (rc != -2) {  // -2: operands beyond the split kernels' 32-bit offsets -> fused form
       check_launch(rc, "attn_bwd_split");
+      if (want_bias) {
+        if (p.bias_part)
+          check_launch(orion_colsum_partials2(p.bias_part, p.bias_part + prow * ld, bias_grad->data_ptr(),
+                                              (int)prow, (int)ld, is_f32(*bias_grad), cur_stream()),
+                       "attn_bias_colsum");
+        else
+          attn_bias_colsum_packed(dq, *bias_grad, p.B * p.T, ld);
+      }
       return;
     }
+    p.bias_part = nullptr;
   }
   auto dq_acc = at::empty({p.B, p.Hq, p.T, D}, fopts);
   p.dq_acc = dq_acc.data_ptr<float>();
@@ -796,6 +839,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   check_launch(orion_attn_dq_convert(dq_acc.data_ptr<float>(), dq.data_ptr(), dq.stride(0),
                                      dq.stride(1), dq.stride(2), p.B, p.Hq, p.T, D, cur_stream()),
                "attn_dq_convert");
+  if (want_bias) attn_bias_colsum_packed(dq, *bias_grad, p.B * p.T, ld);
 }
 
 }  // namespace
@@ -829,7 +873,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int pos0, float sign) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int pos0, float sign) -> ()");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int flags=0) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int flags=0, Tensor(d!)? bias_grad=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {

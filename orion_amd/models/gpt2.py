@@ -74,8 +74,9 @@ class CausalSelfAttention(nn.Module):
         self.dropout = cfg.dropout
 
     def forward(self, x, fuse_out_bias=False):
-        qkv = ops.linear(x, self.c_attn.weight, self.c_attn.bias)     # (B, T, 3C)
-        y = ops.attention_qkv(qkv, self.n_head, causal=True)         # (B, T, C)
+        # QKV projection + attention; the projection's bias gradient is summed inside the
+        # attention backward on the HIP path
+        y = ops.linear_attention_qkv(x, self.c_attn.weight, self.c_attn.bias, self.n_head)  # (B, T, C)
         # with fuse_out_bias the caller adds c_proj.bias inside its add+LayerNorm kernel
         y = ops.linear(y, self.c_proj.weight, None if fuse_out_bias else self.c_proj.bias)
         if self.dropout and self.training:

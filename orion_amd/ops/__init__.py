@@ -213,6 +213,18 @@ def attention_qkv(qkv, n_head, causal=True):
     return ref.attention_qkv(qkv, n_head, causal)
 
 
+def linear_attention_qkv(x, weight, bias, n_head, causal=True):
+    """Causal self-attention of the QKV projection x W^T + b -> (B, T, C).  On the HIP path
+    the projection's bias gradient comes out of the attention backward (column sums fused
+    into the split kernels) instead of a column-sum pass over the packed dQKV."""
+    if _gpu(x) == "hip" and bias is not None:
+        from .flash_attn import flash_attention_qkv
+        from .layernorm import linear_hip
+        qkv = linear_hip(x, weight, bias.detach())
+        return flash_attention_qkv(qkv, n_head, causal, bias)
+    return attention_qkv(linear(x, weight, bias), n_head, causal)
+
+
 def attention(q, k, v, causal=True):
     """Attention on (B, T, H, D) tensors (GQA when k/v have fewer heads)."""
     b = _gpu(q)
@@ -255,5 +267,5 @@ def linear_cross_entropy(x, weight, targets, ignore_index=-1):
 __all__ = [
     "set_backend", "backend", "ext_available", "load_ext",
     "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm", "rope",
-    "attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "linear_cross_entropy",
+    "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "linear_cross_entropy",
 ]

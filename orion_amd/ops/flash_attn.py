@@ -19,8 +19,14 @@ def _bwd_flags() -> int:
 
 
 class _FlashQKV(torch.autograd.Function):
+    """Attention on the packed (B, T, 3C) output of the QKV projection.  ``qkv_bias``: the
+    projection's bias, already added to ``qkv`` by a linear that did not track it; its
+    gradient colsum(dQKV) is produced here -- by the split backward kernels as fp32 column
+    sums per 32-token block (no pass over the packed dQKV) -- and written through the
+    bias's gradient sink (ops/grad_sink.py)."""
+
     @staticmethod
-    def forward(ctx, qkv, n_head, causal):
+    def forward(ctx, qkv, n_head, causal, qkv_bias):
         B, T, C3 = qkv.shape
         Cm = C3 // 3
         D = Cm // n_head
@@ -29,6 +35,7 @@ class _FlashQKV(torch.autograd.Function):
         o, lse = C().attn_fwd(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], bool(causal), scale)
         ctx.save_for_backward(qkv, o, lse)
         ctx.meta = (n_head, bool(causal), scale)
+        ctx.bias = qkv_bias
         return o.view(B, T, Cm)
 
     @staticmethod
@@ -41,13 +48,25 @@ class _FlashQKV(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         d5 = dqkv.view(B, T, 3, n_head, D)
         do4 = do.contiguous().view(B, T, n_head, D)
+        bias = ctx.bias
+        want_db = bias is not None and ctx.needs_input_grad[3]
+        sb = db = None
+        if want_db:
+            from .grad_sink import claim
+            sb = claim(bias) if bias.dtype == torch.bfloat16 else None
+            db = sb.view if sb is not None else torch.empty(C3, dtype=qkv.dtype, device=qkv.device)
         C().attn_bwd(do4, v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], o, lse, causal, scale,
-                     d5[:, :, 0], d5[:, :, 1], d5[:, :, 2], _bwd_flags())
-        return dqkv, None, None
+                     d5[:, :, 0], d5[:, :, 1], d5[:, :, 2], _bwd_flags(), db)
+        if sb is not None:  # written into the arena slice; never handed back to autograd
+            sb.notify()
+            db = None
+        elif db is not None:
+            db = db.to(bias.dtype)
+        return dqkv, None, None, db
 
 
-def flash_attention_qkv(qkv, n_head, causal=True):
-    return _FlashQKV.apply(qkv, n_head, causal)
+def flash_attention_qkv(qkv, n_head, causal=True, qkv_bias=None):
+    return _FlashQKV.apply(qkv, n_head, causal, qkv_bias)
 
 
 class _Flash(torch.autograd.Function):
