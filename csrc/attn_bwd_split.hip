@@ -35,23 +35,53 @@
 namespace orion {
 
 // delta[b][h][t] = sum_d dO * O (D/8 lanes per row, 8 bf16 per lane)
-template <int D>
+//
+// BIAS (packed self-attention, Hq == Hkv, D = 64, T % 32 == 0: a workgroup's 32 rows are one
+// 32-token block of one head): also the QKV bias gradient's K and V column sums of the block.
+// Softmax is invariant to a shift of every key, so sum_keys dK = scale sum_q Q (sum_k dS) = 0
+// (sum_k P (dP - delta) = delta - delta); and sum_keys dV = sum_q dO (sum_k P) = sum_q dO.
+// The K columns get 0 and the V columns the block's column sum of dO: the dK/dV kernel
+// needs no reduction of its own.
+template <int D, bool BIAS = false>
 __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* __restrict__ delta) {
   constexpr int TPR = D / 8;
   const long row = (blockIdx.x * 256L + threadIdx.x) / TPR;
   const int sub = threadIdx.x % TPR;
   const long nrows = (long)p.B * p.Hq * p.T;
   float s = 0.f;
+  [[maybe_unused]] bf16x8 d;
   if (row < nrows) {
     const long t = row % p.T, h = (row / p.T) % p.Hq, b = row / ((long)p.T * p.Hq);
     const bf16x8 o = *reinterpret_cast<const bf16x8*>(p.o + b * p.o_sb + h * p.o_sh + t * p.o_st + sub * 8);
-    const bf16x8 d = *reinterpret_cast<const bf16x8*>(p.dout + b * p.do_sb + h * p.do_sh + t * p.do_st + sub * 8);
+    d = *reinterpret_cast<const bf16x8*>(p.dout + b * p.do_sb + h * p.do_sh + t * p.do_st + sub * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += bf2f(o[j]) * bf2f(d[j]);
   }
 #pragma unroll
   for (int o2 = TPR / 2; o2 > 0; o2 >>= 1) s += __shfl_xor(s, o2, 64);
   if (row < nrows && sub == 0) delta[row] = s;
+  if constexpr (BIAS) {
+    static_assert(D == 64, "one 32-row block per workgroup");
+    __shared__ float red[32][D + 1];
+    const int r = threadIdx.x / TPR;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[r][sub * 8 + j] = row < nrows ? bf2f(d[j]) : 0.f;
+    __syncthreads();
+    const long row0 = blockIdx.x * 32L;  // first row of the block: (b, h, t0), t0 % 32 == 0
+    if (row0 < nrows && threadIdx.x < 2 * D) {
+      const long t0 = row0 % p.T, h = (row0 / p.T) % p.Hq, b = row0 / ((long)p.T * p.Hq);
+      float* prow = p.bias_part + (b * (p.T / 32) + t0 / 32) * p.bias_ld + (p.Hq + h) * D;
+      const int c = threadIdx.x & (D - 1);
+      if (threadIdx.x < D) {
+        prow[c] = 0.f;  // K columns
+      } else {
+        float cs = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) cs += red[i][c];
+        prow[p.Hkv * D + c] = cs;  // V columns
+      }
+    }
+  }
 }
 
 // 16 bytes per lane by a raw buffer load (scalar soffset carries the tile position)
@@ -110,8 +140,8 @@ __host__ __device__ constexpr int kv_waves() { return 4; }
 // s_memtime deltas of the five phases of a query tile (S/dP chain issue, softmax, dV/dK
 // issue, LDS stage write, barrier) and writes them with its active-tile count and lifetime
 // over p.dq (the dQ kernel is then skipped): scripts/attn_stamps.py, profiles/attn_r03/.
-template <int D, bool CAUSAL, bool STAMPS = false, bool BIAS = false>
-__global__ __launch_bounds__(kv_waves<D>() * 64, BIAS ? 3 : 2) void attn_bwd_kv_kernel(AttnParams p) {
+template <int D, bool CAUSAL, bool STAMPS = false>
+__global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
   constexpr int NW = kv_waves<D>(), NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
   constexpr int QT = BMQ * D;            // Q / dO tile elements
@@ -358,13 +388,6 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, BIAS ? 3 : 2) void attn_bwd_kv_
   }
 
   // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
-  if (BIAS && kw0 < p.Tk) {  // column sums of this wave's 32 keys (packed QKV bias grad)
-    float* row = p.bias_part + ((long)b * ((p.Tk + 31) / 32) + kw0 / 32) * p.bias_ld + (p.Hq + hk) * D;
-    wave_colsum_store<NDB>(dka, p.scale, mykey < p.Tk, l32, h32, row);
-    __builtin_amdgcn_sched_barrier(0);
-    wave_colsum_store<NDB>(dva, 1.f, mykey < p.Tk, l32, h32, row + p.Hkv * D);
-    __builtin_amdgcn_sched_barrier(0);
-  }
   if (mykey < p.Tk) {
     bf16_t* dKb = p.dk + b * p.dk_sb + hk * p.dk_sh + (long)mykey * p.dk_st;
     bf16_t* dVb = p.dv + b * p.dv_sb + hk * p.dv_sh + (long)mykey * p.dv_st;
@@ -596,8 +619,6 @@ template <bool CAUSAL>
 static void bias_attrs() {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<64, CAUSAL, false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(64));
     (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<64, CAUSAL, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(64));
     done = true;
@@ -650,13 +671,13 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
     }
     return (int)hipGetLastError();
   }
-  if (p.bias_part) {  // packed self-attention with the QKV bias gradient (GPT-2: D = 64)
-    if (D != 64 || fused || p.T != p.Tk) return -3;
-    q.bias_part = p.bias_part;
+  if (p.bias_part) {  // packed self-attention with the QKV bias gradient (GPT-2: D = 64, MHA)
+    if (D != 64 || fused || p.T != p.Tk || p.Hq != p.Hkv || p.T % 32) return -3;
 #define SPLITB(CC)                                                                                  \
+  split_attrs<64, CC>();                                                                            \
   bias_attrs<CC>();                                                                                 \
-  attn_delta_kernel<64><<<pre_grid, 256, 0, st>>>(p, delta);                                        \
-  attn_bwd_kv_kernel<64, CC, false, true><<<kv_grid, kv_waves<64>() * 64, kv_lds(64), st>>>(q);     \
+  attn_delta_kernel<64, true><<<pre_grid, 256, 0, st>>>(q, delta);                                  \
+  attn_bwd_kv_kernel<64, CC><<<kv_grid, kv_waves<64>() * 64, kv_lds(64), st>>>(q);                  \
   attn_bwd_dq_kernel<64, CC, false, true><<<dq_grid, 256, dq_lds(64), st>>>(q);
     if (causal) { SPLITB(true) } else { SPLITB(false) }
 #undef SPLITB

@@ -28,9 +28,10 @@ struct AttnParams {
   unsigned short* dq;  // bf16 dQ (split backward: written directly, no fp32 accumulator)
   long dq_sb, dq_st, dq_sh;
   int flags;  // 1 = skip dQ atomics (diagnostic), 4 = deterministic (split backward), 8 = fused
-  // split backward, packed self-attention (T == Tk): column sums of dQ | dK | dV over every
-  // 32-row block of tokens, [B * ceil(T / 32)][bias_ld] fp32 (bias_ld = (Hq + 2 Hkv) D), so the
-  // QKV projection's bias gradient needs no pass over the packed dQKV
+  // split backward, packed self-attention (T == Tk, MHA, D = 64, T % 32 == 0): column sums of
+  // dQ | dK | dV over every 32-token block, [B * T / 32][bias_ld] fp32 (bias_ld = 3 Hq D) -- dQ's
+  // from the dQ kernel, dK's (identically 0) and dV's (= those of dO) from the delta pass -- so
+  // the QKV projection's bias gradient needs no pass over the packed dQKV
   float* bias_part;
   int bias_ld;
 };

@@ -766,9 +766,11 @@ bool attn_bwd_use_split(int D, int64_t flags) {
 
 // dq/dk/dv: preallocated outputs (may be strided views of one packed buffer)
 // bias_grad (optional): the QKV projection's bias gradient, colsum over tokens of the packed
-// (B, T, Hq + 2 Hkv, D) dQKV that dq / dk / dv must then be views of.  The split kernels sum
-// their fp32 outputs per 32-token block (AttnParams::bias_part) and a two-stage fold writes
-// bias_grad (fp32 arena slice or bf16); other backward forms sum the packed bf16 dQKV.
+// (B, T, Hq + 2 Hkv, D) dQKV that dq / dk / dv must then be views of.  The split form (MHA,
+// D = 64, T % 32 == 0) produces fp32 column sums per 32-token block (AttnParams::bias_part:
+// dQ's in the dQ kernel, dK's = 0 and dV's = colsum(dO) in the delta pass) and a two-stage
+// fold writes bias_grad (fp32 arena slice or bf16); other shapes and forms sum the packed
+// bf16 dQKV.
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
               const Tensor& o, const Tensor& lse, bool causal, double scale, Tensor dq, Tensor dk,
               Tensor dv, int64_t flags, const c10::optional<Tensor>& bias_grad) {

@@ -87,6 +87,8 @@ def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
 
 
 def _hip_wins(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
+    # short-K forwards (GPT-2 qkv / attn-proj) in-tree with the packed bias epilogue measured
+    # 0.7-0.9 % slower end to end (profiles/ab/ab_fwd_shortk_r03o.log): forwards stay on hipBLASLt
     return w_kmajor
 
 

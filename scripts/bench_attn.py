@@ -66,6 +66,14 @@ def main():
                                                                dq, dk, dv, 9))
     res["bwd_split_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, causal, scale, dq, dk, dv, 4))
     res["bwd_ms"] = min(res["bwd_fused_ms"], res["bwd_split_ms"])
+    if Hkv == H and D == 64:  # packed QKV with the bias gradient summed in the split kernels
+        d5 = dqkv.view(B, T, 3, H, D)
+        db = torch.empty(3 * H * D, device="cuda", dtype=torch.float32)
+        res["bwd_split_bias_ms"] = timeit(lambda: ops.attn_bwd(do, q, k, v, o, lse, causal, scale, d5[:, :, 0],
+                                                               d5[:, :, 1], d5[:, :, 2], 4, db))
+        res["bwd_split_plus_colsum_ms"] = timeit(lambda: (ops.attn_bwd(do, q, k, v, o, lse, causal, scale, d5[:, :, 0],
+                                                                       d5[:, :, 1], d5[:, :, 2], 4),
+                                                          ops.colsum(dqkv.view(B * T, -1), db)))
     res["fwd_TFs"] = 2 * flops_mm / res["fwd_ms"] / 1e9
     res["bwd_TFs"] = 5 * flops_mm / res["bwd_ms"] / 1e9
     res["bwd_over_fwd"] = res["bwd_ms"] / res["fwd_ms"]

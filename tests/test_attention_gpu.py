@@ -210,15 +210,16 @@ def test_split_backward_delta_modes_match(tmp_path):
 
 
 @pytest.mark.parametrize("form", [0, SPLIT, FUSED])
-@pytest.mark.parametrize("D,Hq,Hkv", [(64, 4, 4), (64, 4, 2), (128, 4, 2)])
+@pytest.mark.parametrize("D,Hq,Hkv,T", [(64, 4, 4, 256), (64, 4, 4, 200), (64, 4, 2, 256), (128, 4, 2, 256)])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-def test_packed_qkv_bias_grad_matches_colsum(form, D, Hq, Hkv, causal, out_dtype):
+def test_packed_qkv_bias_grad_matches_colsum(form, D, Hq, Hkv, T, causal, out_dtype):
     """attn_bwd(..., bias_grad=out) on a packed (B, T, Hq + 2 Hkv, D) dQKV: the QKV bias
-    gradient colsum(dQKV) -- from the split kernels' fp32 per-32-token column sums at D = 64,
-    from a column sum of the packed bf16 dQKV otherwise -- matches the fp32 column sum of
-    the reference gradients; dQKV itself equals the call without the bias output."""
-    B, T = 2, 200  # T not a multiple of 32: the last token block is partial
+    gradient colsum(dQKV) -- from the split kernels' fp32 per-32-token column sums (MHA,
+    D = 64, T % 32 == 0: dQ's from the dQ kernel, dK's = 0 and dV's = colsum(dO) from the
+    delta pass), from a column sum of the packed bf16 dQKV otherwise -- matches the fp32
+    column sum of the reference gradients; dQKV equals the call without the bias output."""
+    B = 2
     C = _C()
     g = torch.Generator(device=DEV).manual_seed(5)
     qkv = torch.randn(B, T, Hq + 2 * Hkv, D, device=DEV, dtype=torch.bfloat16, generator=g)
