@@ -382,32 +382,52 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   constexpr bool CS = EPI == EPI_GELU_BWD;
   // bf16 pair word -> two floats (low half first)
   auto unpack2 = [](unsigned w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)}; };
+  // Every epilogue operand (bias, GELU' pre-activations) is loaded up front, before the first
+  // store: a load after a store is kept behind it (they may alias) and then waited with
+  // vmcnt(0), which on CDNA4 also waits for the stores -- the GELU' epilogue ran as 17
+  // serial HBM round trips per wave.  The fragment registers of the main loop are dead here.
+  auto ncol = [&](int ap) { return nw + 16 * (2 * ap + (q & 1)) + 8 * (q >> 1); };
+  [[maybe_unused]] u32x4 bias4[4];
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_GELU_BWD) {
+#pragma unroll
+    for (int ap = 0; ap < 4; ++ap) {
+      const int nb = ncol(ap), nc = nb < g.N ? nb : 0;
+      if (EPI != EPI_GELU_BWD || g.bias) bias4[ap] = *reinterpret_cast<const u32x4*>(g.bias + nc);
+      else bias4[ap] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  [[maybe_unused]] u32x4 pre4[4][4];
+  if constexpr (EPI == EPI_GELU_BWD) {
+    const __amdgpu_buffer_rsrc_t rp =
+        make_rsrc(g.pre + (long)m0 * g.ldp, (unsigned)(((long)(rows_m - 1) * g.ldp + g.N) * 2));
+#pragma unroll
+    for (int ap = 0; ap < 4; ++ap) {
+      const int nb = ncol(ap), nc = nb < g.N ? nb : 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int mc = min(mw + 16 * b + i16, g.M - 1);
+        pre4[ap][b] = __builtin_amdgcn_raw_buffer_load_b128(rp, (unsigned)(((long)(mc - m0) * g.ldp + nc) * 2), 0, 0);
+      }
+    }
+  }
   // the value arithmetic runs on pairs of adjacent columns (v_pk_*_f32: no MFMA issues beside
   // the epilogue) and every pair is packed to bf16 by one v_cvt_pk_bf16_f32
 #pragma unroll
   for (int ap = 0; ap < 4; ++ap) {
     // after the swap: lane (q, i16) holds n = nb .. nb + 7 of row m (fp32)
-    const int nb = nw + 16 * (2 * ap + (q & 1)) + 8 * (q >> 1);
+    const int nb = ncol(ap);
     const bool nok = nb < g.N;
-    const int nc = nok ? nb : 0;
     [[maybe_unused]] f32x2 bias[4];
     if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_GELU_BWD) {
-      if (EPI != EPI_GELU_BWD || g.bias) {
-        const u32x4 b4 = *reinterpret_cast<const u32x4*>(g.bias + nc);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bias[e] = unpack2(b4[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bias[e] = splat2(0.f);
-      }
+      for (int e = 0; e < 4; ++e) bias[e] = unpack2(bias4[ap][e]);
     }
     [[maybe_unused]] f32x2 cs[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int m = mw + 16 * b + i16;
-      const int mc = min(m, g.M - 1);
       [[maybe_unused]] u32x4 p4;
-      if constexpr (EPI == EPI_GELU_BWD) p4 = *reinterpret_cast<const u32x4*>(g.pre + (long)mc * g.ldp + nc);
+      if constexpr (EPI == EPI_GELU_BWD) p4 = pre4[ap][b];
       f32x2 v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -506,9 +526,9 @@ static int gemm16_launch(const GemmArgs& a, hipStream_t st) {
 bool gemm16_ok(const GemmArgs& a, int wkm) {
   const long lim = 0xFFFFFF00L;
   const long band = 256L * (a.ldx > a.ldw ? a.ldx : a.ldw) * 2;
-  const long ob = 256L * (a.ldo > a.ldo2 ? a.ldo : a.ldo2) * 2;
+  const long ob = 256L * (a.ldo > a.ldo2 ? a.ldo : a.ldo2) * 2, pb = 256L * a.ldp * 2;
   const long wb = wkm ? (long)a.K * a.ldw * 2 : 0;
-  return band < lim && ob < lim && wb < lim;
+  return band < lim && ob < lim && pb < lim && wb < lim;
 }
 
 int gemm16_wgrad(const GemmArgs& a, hipStream_t st) {
