@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 }
 
 // Backward: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma.
-template <int VEC, int ITERS>
+template <int VEC, int ITERS, bool EXACT = false>  // EXACT: ITERS * 64 * VEC == C (no column guards)
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -142,71 +142,75 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   typedef typename VecT<VEC>::type V;
-  // Two rows per wave per iteration, every load of both rows (x, dy, and the
-  // residual-stream gradient) issued before the first reduction: each wave keeps
-  // 2x the bytes in flight and the dres load no longer sits behind the shuffles.
-  constexpr int RU = 2;
-  for (int row = r0 + wv; row < r1; row += 4 * RU) {
-    V xr[RU][ITERS], dyr[RU][ITERS], rr[RU][ITERS];
+  // One row per wave per step, software-pipelined over two register sets: the loads of the
+  // wave's next row are issued BEFORE this row's dx stores.  On CDNA4 vmcnt counts stores
+  // too, so a load issued after a store is waited for behind that store's completion; with
+  // the loads of row r + 4 ahead of the stores of row r, the wait for them leaves the
+  // stores in flight (the two-rows-then-stores form serialised every step on its stores).
+  auto load_row = [&](int rw, V (&xr)[ITERS], V (&dyr)[ITERS], V (&rr)[ITERS]) {
+    if (rw >= r1) return;  // wave-uniform
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int rw = row + 4 * u;
-#pragma unroll
-      for (int i = 0; i < ITERS; ++i) {
-        const int c = (i * 64 + lane) * VEC;
-        if (c < C && rw < r1) {
-          xr[u][i] = *reinterpret_cast<const V*>(x + (size_t)rw * C + c);
-          dyr[u][i] = *reinterpret_cast<const V*>(dy + (size_t)rw * C + c);
-          if (dres) rr[u][i] = *reinterpret_cast<const V*>(dres + (size_t)rw * C + c);
-        }
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (EXACT || c < C) {
+        xr[i] = *reinterpret_cast<const V*>(x + (size_t)rw * C + c);
+        dyr[i] = *reinterpret_cast<const V*>(dy + (size_t)rw * C + c);
+        if (dres) rr[i] = *reinterpret_cast<const V*>(dres + (size_t)rw * C + c);
       }
     }
+  };
+  auto proc_row = [&](int rw, const V (&xr)[ITERS], const V (&dyr)[ITERS], const V (&rr)[ITERS]) {
+    const float mean = mean_in[rw], rstd = rstd_in[rw];
+    float xh[ITERS][VEC], g[ITERS][VEC];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int rw = row + 4 * u;
-      if (rw >= r1) break;
-      const float mean = mean_in[rw], rstd = rstd_in[rw];
-      float xh[ITERS][VEC], g[ITERS][VEC];
-      float s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (EXACT || c < C) {
 #pragma unroll
-      for (int i = 0; i < ITERS; ++i) {
-        const int c = (i * 64 + lane) * VEC;
-        if (c < C) {
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) {
-            const float dv = bf2f(dyr[u][i][j]);
-            xh[i][j] = (bf2f(xr[u][i][j]) - mean) * rstd;
-            g[i][j] = dv * wf[i][j];
-            s1 += g[i][j];
-            s2 += g[i][j] * xh[i][j];
-            adw[i][j] += dv * xh[i][j];
-            adb[i][j] += dv;
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) { xh[i][j] = 0.f; g[i][j] = 0.f; }
+        for (int j = 0; j < VEC; ++j) {
+          const float dv = bf2f(dyr[i][j]);
+          xh[i][j] = (bf2f(xr[i][j]) - mean) * rstd;
+          g[i][j] = dv * wf[i][j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+          adw[i][j] += dv * xh[i][j];
+          adb[i][j] += dv;
         }
-      }
-      const float m1 = wave_sum(s1) * invC, m2 = wave_sum(s2) * invC;
-      bf16_t* dxr = dx + (size_t)rw * C;
+      } else {
 #pragma unroll
-      for (int i = 0; i < ITERS; ++i) {
-        const int c = (i * 64 + lane) * VEC;
-        if (c < C) {
-          float o[VEC];
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) {
-            o[j] = rstd * (g[i][j] - m1 - xh[i][j] * m2);
-            if (dres) o[j] += bf2f(rr[u][i][j]);  // gradient arriving through the residual stream
-          }
-          if (part_dx) {
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) adx[i][j] += bf2f(f2bf(o[j]));
-          }
-          store_vec<VEC>(dxr + c, o);
-        }
+        for (int j = 0; j < VEC; ++j) { xh[i][j] = 0.f; g[i][j] = 0.f; }
       }
     }
+    const float m1 = wave_sum(s1) * invC, m2 = wave_sum(s2) * invC;
+    bf16_t* dxr = dx + (size_t)rw * C;
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (EXACT || c < C) {
+        float o[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          o[j] = rstd * (g[i][j] - m1 - xh[i][j] * m2);
+          if (dres) o[j] += bf2f(rr[i][j]);  // gradient arriving through the residual stream
+        }
+        if (part_dx) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) adx[i][j] += bf2f(f2bf(o[j]));
+        }
+        store_vec<VEC>(dxr + c, o);
+      }
+    }
+  };
+  V xa[ITERS], da[ITERS], ra[ITERS], xb[ITERS], db[ITERS], rb[ITERS];
+  int row = r0 + wv;
+  load_row(row, xa, da, ra);
+  for (; row < r1; row += 8) {
+    load_row(row + 4, xb, db, rb);
+    proc_row(row, xa, da, ra);
+    if (row + 4 >= r1) break;
+    load_row(row + 8, xa, da, ra);
+    proc_row(row + 4, xb, db, rb);
   }
   // fold the 4 waves' column partials through LDS, one output pass per quantity
   if (part_dw) {
@@ -465,6 +469,13 @@ int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const floa
       case 2: ln_bwd_kernel<8, 2><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
       case 3: ln_bwd_kernel<8, 3><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
       case 4: ln_bwd_kernel<8, 4><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+    }
+  } else if (C == it * 256) {  // exact fit (GPT-2: C = 768): no column guards
+    switch (it) {
+      case 1: ln_bwd_kernel<4, 1, true><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 2: ln_bwd_kernel<4, 2, true><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 3: ln_bwd_kernel<4, 3, true><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
+      case 4: ln_bwd_kernel<4, 4, true><<<nb, 256, lds, st>>>(DY, X, W, mean, rstd, DX, pdw, pdb, rows, C, rpb, DR, pdx); break;
     }
   } else {
     switch (it) {

@@ -57,6 +57,16 @@ def main():
     tg = torch.randint(0, V, (R,), device=dev)
     rec("xent", timeit(lambda: ops.xent_fwd_bwd(logits, tg, -1), a.iters), 2 * R * V * 2)
     del logits
+    # flat AdamW over a GPT-2-124M-sized arena (fp32 grads, master, m, v; bf16 weights)
+    n = 124 * 1024 * 1024
+    p16 = torch.zeros(n, device=dev, dtype=bf)
+    master, mm, vv, gg = (torch.randn(n, device=dev) * 0.01 for _ in range(4))
+    vv.abs_()
+    decay = torch.ones(n // 2048, device=dev, dtype=torch.uint8)
+    hyper = torch.tensor([6e-4, 0.9, 0.95, 1e-8, 0.1, 0.1, 0.05, 1.0], device=dev)
+    ssq = torch.ones(1, device=dev)
+    rec("adamw", timeit(lambda: ops.adamw_flat(p16, master, mm, vv, gg, decay, hyper, ssq), a.iters), n * 30)
+    del p16, master, mm, vv, gg
     res.update(rows=R, C=Cc, V=V)
     print(json.dumps(res), flush=True)
 
