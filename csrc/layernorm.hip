@@ -55,21 +55,40 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   }
   const bf16_t* xr = x + (size_t)id * C;
   const size_t rrow = idx ? (size_t)(row % T) : (size_t)row;
+  // Every load of the row (x, residual, branch bias, gamma, beta) is issued, unconditionally
+  // and as raw bf16 vectors, before the first store: on CDNA4 vmcnt counts stores, so a load
+  // after the sum store would wait for it, and per-operand branches (or conversions right
+  // after each load) made the compiler wait for every load in turn.  Absent operands read a
+  // stand-in row, columns past C the last chunk (their results are not stored).
+  typedef typename VecT<VEC>::type VT;
+  const bf16_t* rp = res ? res + rrow * C : xr;
+  const bf16_t* rbp = (res && rbias) ? rbias : w;
+  const bf16_t* bp = b ? b : w;
+  VT xv[ITERS], rvv[ITERS], rbv[ITERS], wv[ITERS], bvv[ITERS];
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int cl = min((i * 64 + lane) * VEC, C - VEC);
+    xv[i] = *reinterpret_cast<const VT*>(xr + cl);
+    rvv[i] = *reinterpret_cast<const VT*>(rp + cl);
+    rbv[i] = *reinterpret_cast<const VT*>(rbp + cl);
+    wv[i] = *reinterpret_cast<const VT*>(w + cl);
+    bvv[i] = *reinterpret_cast<const VT*>(bp + cl);
+  }
   float v[ITERS][VEC];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
     const int c = (i * 64 + lane) * VEC;
     if (c < C) {
-      load_vec<VEC>(xr + c, v[i]);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) v[i][j] = bf2f(xv[i][j]);
       if (res) {  // fused residual add: s = x + r is both returned and normalised
         float rv[VEC];
-        load_vec<VEC>(res + rrow * C + c, rv);
-        if (rbias) {  // the branch's output-projection bias, added here instead of in the GEMM
-          float bv[VEC];
-          load_vec<VEC>(rbias + c, bv);
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) rv[j] = bf2f(f2bf(rv[j] + bv[j]));
+        for (int j = 0; j < VEC; ++j) rv[j] = bf2f(rvv[i][j]);
+        if (rbias) {  // the branch's output-projection bias, added here instead of in the GEMM
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) rv[j] = bf2f(f2bf(rv[j] + bf2f(rbv[i][j])));
         }
 #pragma unroll
         for (int j = 0; j < VEC; ++j) v[i][j] = bf2f(f2bf(v[i][j] + rv[j]));
@@ -102,11 +121,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   for (int i = 0; i < ITERS; ++i) {
     const int c = (i * 64 + lane) * VEC;
     if (c < C) {
-      float wf[VEC], bfv[VEC], o[VEC];
-      load_vec<VEC>(w + c, wf);
-      if (b) load_vec<VEC>(b + c, bfv);
+      float o[VEC];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) o[j] = (v[i][j] - mean) * rstd * wf[j] + (b ? bfv[j] : 0.f);
+      for (int j = 0; j < VEC; ++j) o[j] = (v[i][j] - mean) * rstd * bf2f(wv[i][j]) + (b ? bf2f(bvv[i][j]) : 0.f);
       store_vec<VEC>(yr + c, o);
     }
   }
