@@ -267,5 +267,6 @@ def linear_cross_entropy(x, weight, targets, ignore_index=-1):
 __all__ = [
     "set_backend", "backend", "ext_available", "load_ext",
     "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm", "rope",
-    "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "linear_cross_entropy",
+    "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy",
+    "linear_cross_entropy",
 ]
