@@ -62,7 +62,8 @@ def main(argv=None):
     kw = dict(gpus_per_trial=execution.get("gpus_per_trial", 0),
               heartbeat=execution.get("heartbeat", 30.0),
               trial_timeout=execution.get("trial_timeout"),
-              max_broken=execution.get("max_broken", 3))
+              max_broken=execution.get("max_broken", 3),
+              trial_runner=execution.get("trial_runner") or "exec")
     n = int(execution.get("workers", 1) or 1)
     if n > 1:
         # a crashed worker process makes the CLI fail instead of reporting success

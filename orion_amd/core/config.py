@@ -131,6 +131,9 @@ def build_parser(description=CLI_DOC_HEADER):
                     help="liveness period of reserved trials (stale ones are re-queued)")
     xg.add_argument("--max-broken", type=int, metavar="#",
                     help="stop the worker after this many broken trials (default 3)")
+    xg.add_argument("--trial-runner", choices=("exec", "fork"),
+                    help="exec: a new process per trial (default); fork: .py trials forked from a "
+                         "per-worker server that imported torch once (orion_amd/core/forkserver.py)")
     ug = parser.add_argument_group(
         "User script related arguments",
         description="These arguments determine user's script behaviour "
@@ -143,7 +146,7 @@ def build_parser(description=CLI_DOC_HEADER):
     return parser
 
 
-_EXEC_KEYS = ("workers", "gpus_per_trial", "trial_timeout", "heartbeat", "max_broken")
+_EXEC_KEYS = ("workers", "gpus_per_trial", "trial_timeout", "heartbeat", "max_broken", "trial_runner")
 
 
 def fetch_orion_args(description=CLI_DOC_HEADER, argv=None):

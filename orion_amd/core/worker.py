@@ -28,17 +28,26 @@ log = logging.getLogger(__name__)
 
 
 def workon(experiment, gpus_per_trial=0, heartbeat=30.0, trial_timeout=None, max_broken=3,
-           worker_id=None, gpu_pool=None, idle_sleep=(0.01, 1.0)):
+           worker_id=None, gpu_pool=None, idle_sleep=(0.01, 1.0), trial_runner="exec"):
     """Run the produce/consume loop until the experiment is done.  Returns its stats."""
-    worker_id = worker_id or f"{socket.gethostname()}:{os.getpid()}"
-    producer = Producer(experiment)
     consumer = Consumer(experiment, gpu_pool=gpu_pool, gpus_per_trial=gpus_per_trial,
-                        heartbeat=heartbeat, trial_timeout=trial_timeout, worker_id=worker_id)
+                        heartbeat=heartbeat, trial_timeout=trial_timeout,
+                        worker_id=worker_id or f"{socket.gethostname()}:{os.getpid()}",
+                        trial_runner=trial_runner)
+    try:
+        return _workon(experiment, consumer, max_broken, idle_sleep)
+    finally:
+        consumer.close()
+
+
+def _workon(experiment, consumer, max_broken, idle_sleep):
+    worker_id = consumer.worker_id
+    producer = Producer(experiment)
     broken = 0
     sleep = idle_sleep[0]
     # a reservation whose heartbeat is older than this is re-queued (floor: 30 s, or
     # ORION_STALE_AFTER_MIN_S for tests that exercise the reaper)
-    stale_after = max(3 * heartbeat, float(os.environ.get("ORION_STALE_AFTER_MIN_S", "30")))
+    stale_after = max(3 * consumer.heartbeat, float(os.environ.get("ORION_STALE_AFTER_MIN_S", "30")))
     log.debug("#####  Init Experiment  #####")
     budgeted = experiment.max_trials not in (None, float("inf"))
     while True:

@@ -22,15 +22,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 ORION = [sys.executable, os.path.join(ROOT, "bin", "orion")]
 
 
-def test_two_workers_share_one_gpu_lease(tmp_path):
+@pytest.mark.parametrize("runner", ["exec", "fork"])
+def test_two_workers_share_one_gpu_lease(tmp_path, runner):
     db = str(tmp_path / "orion.sqlite")
     env = dict(os.environ, METAOPT_DB_ADDRESS=db, METAOPT_DB_TYPE="sqlite",
                XDG_CONFIG_HOME=str(tmp_path), ORION_GPUS="0",
                TMPDIR=str(tmp_path))  # private lease-lock directory for this test
     out = tmp_path / "out"
     t0 = time.time()
-    rc = subprocess.call(ORION + ["-n", "gpu-smoke", "--max-trials", "4", "--workers", "2",
-                                  "--gpus-per-trial", "1", "--pool-size", "4", os.path.join(ROOT, "train.py"),
+    rc = subprocess.call(ORION + ["-n", "gpu-smoke", "--max-trials", "8", "--workers", "2",
+                                  "--gpus-per-trial", "1", "--pool-size", "4", "--trial-runner", runner,
+                                  os.path.join(ROOT, "train.py"),
                                   "--device=cuda", "--model=gpt2-tiny", "--block_size=64",
                                   "--batch_size=8", "--gradient_accumulation_steps=1",
                                   "--max_iters=20", "--eval_interval=20", "--eval_iters=2",
@@ -43,9 +45,9 @@ def test_two_workers_share_one_gpu_lease(tmp_path):
     (exp,) = store.read("experiments", {"name": "gpu-smoke"})
     trials = store.read("trials", {"experiment": exp["_id"]})
     done = [t for t in trials if t["status"] == "completed"]
-    # the trial budget holds: --max-trials 4 with 2 workers and --pool-size 4 runs exactly 4
-    # trainings (round 2 ran 8: every idle worker registered a whole pool)
-    assert len(trials) == 4 and len(done) == 4, [t["status"] for t in trials]
+    # the trial budget holds: --max-trials 8 with 2 workers and --pool-size 4 runs exactly 8
+    # trainings (round 2 ran twice the budget: every idle worker registered a whole pool)
+    assert len(trials) == 8 and len(done) == 8, [t["status"] for t in trials]
     for t in done:
         (r,) = [r for r in t["results"] if r["type"] == "objective"]
         assert r["value"] > 0
@@ -57,12 +59,12 @@ def test_two_workers_share_one_gpu_lease(tmp_path):
         assert s1 >= e0 - 0.01, "two trials held the single GPU lease at the same time"
     durs = [e - s for s, e in spans]
     busy = sum(durs)
-    rec = {"trials": len(done), "workers": 2, "gpus": 1, "wall_s": round(wall, 2),
+    rec = {"runner": runner, "trials": len(done), "workers": 2, "gpus": 1, "wall_s": round(wall, 2),
            "trials_per_hour": round(len(done) / wall * 3600, 1),
            "trial_s_median": round(sorted(durs)[len(durs) // 2], 2),
            "lease_idle_s": round(max(0.0, (spans[-1][1] - spans[0][0]) - busy), 2),
            "cli_overhead_s": round(wall - (spans[-1][1] - spans[0][0]), 2)}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "hpo_gpu.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"hpo_gpu_{runner}.json"), "w") as f:
         json.dump(rec, f)
     print(json.dumps(rec))

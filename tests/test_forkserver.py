@@ -1,0 +1,148 @@
+"""Fork-server trial runner (``--trial-runner fork``, orion_amd/core/forkserver.py): the
+forked trial honours the subprocess contract the consumer relies on -- exit status
+(SystemExit codes, uncaught exception -> 1, killed -> -signal), environment / argv /
+working directory, its own session for killpg, timeouts -- holds the GPU lease's lock
+descriptors for exactly as long as it lives, and drives complete / broken / timed-out
+trials through the Consumer and the CLI."""
+import os
+import signal
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+from orion_amd.core.consumer import Consumer
+from orion_amd.core.experiment import Experiment
+from orion_amd.core.forkserver import ForkServer
+from orion_amd.core.gpus import GPUSlotPool
+from orion_amd.core.producer import Producer
+from orion_amd.store import Database
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def server():
+    fs = ForkServer(preload=("numpy",))
+    yield fs
+    fs.close()
+
+
+def _script(tmp_path, name, body):
+    p = tmp_path / name
+    p.write_text(textwrap.dedent(body))
+    return str(p)
+
+
+def test_exit_status_env_argv_cwd(server, tmp_path):
+    out = tmp_path / "out.txt"
+    s = _script(tmp_path, "s.py", f"""
+        import os, sys
+        open({str(out)!r}, "w").write(" ".join([os.environ["X"], os.getcwd(), *sys.argv[1:], __name__]))
+        sys.exit(int(sys.argv[1]))
+    """)
+    p = server.spawn([s, "3", "a b"], dict(os.environ, X="hello"), cwd=str(tmp_path))
+    assert p.wait(timeout=30) == 3
+    assert out.read_text() == f"hello {tmp_path} 3 a b __main__"
+    assert server.spawn([s, "0", "x"], dict(os.environ, X="y"), cwd=str(tmp_path)).wait(timeout=30) == 0
+
+
+@pytest.mark.parametrize("body,rc", [("raise ValueError('boom')", 1), ("import sys; sys.exit('msg')", 1),
+                                     ("import sys; sys.exit()", 0)])
+def test_failures_map_to_exit_codes(server, tmp_path, body, rc):
+    s = _script(tmp_path, "f.py", body)
+    assert server.spawn([s], dict(os.environ), cwd=str(tmp_path)).wait(timeout=30) == rc
+
+
+def test_timeout_and_killpg(server, tmp_path):
+    s = _script(tmp_path, "hang.py", """
+        import subprocess, sys, time
+        subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+        time.sleep(60)
+    """)
+    p = server.spawn([s], dict(os.environ), cwd=str(tmp_path))
+    with pytest.raises(subprocess.TimeoutExpired):
+        p.wait(timeout=0.5)
+    assert os.getpgid(p.pid) == p.pid  # its own session: killpg reaches its children too
+    os.killpg(p.pid, signal.SIGTERM)
+    assert p.wait(timeout=30) == -signal.SIGTERM
+
+
+def test_lease_is_held_by_the_forked_trial(server, tmp_path):
+    lock_dir = str(tmp_path / "locks")
+    pool = GPUSlotPool(["0"], lock_dir)
+    lease = pool.try_acquire(1)
+    s = _script(tmp_path, "sleep.py", "import time; time.sleep(1.5)")
+    p = server.spawn([s], dict(os.environ), cwd=str(tmp_path), pass_fds=lease.fds)
+    for fd in lease.fds:  # the worker dies (its descriptors close, no unlock): the trial's
+        os.close(fd)      # copies keep the device locked
+    lease._fds = []
+    assert GPUSlotPool(["0"], lock_dir).try_acquire(1) is None
+    assert p.wait(timeout=30) == 0
+    again = GPUSlotPool(["0"], lock_dir).try_acquire(1)
+    assert again is not None
+    again.release()
+
+
+def _experiment(tmp_path, body, max_trials=3):
+    script = tmp_path / "bb.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, sys
+        sys.path.insert(0, {ROOT!r})
+        from orion_amd.client import report_results
+        {body}
+        report_results([dict(name="o", type="objective", value=float(os.getpid()))])
+    """))
+    exp = Experiment("fork", Database("memory"), user="u")
+    cfg = exp.configuration
+    cfg.update(algorithms={"random": {}}, pool_size=1, max_trials=max_trials)
+    cfg["metadata"]["user_script"] = str(script)
+    cfg["metadata"]["user_args"] = ["-x~uniform(0, 1)"]
+    exp.configure(cfg)
+    Producer(exp).produce()
+    return exp
+
+
+@pytest.mark.parametrize("body,status,timeout", [("pass", "completed", None),
+                                                 ("raise RuntimeError('bad trial')", "broken", None),
+                                                 ("import time; time.sleep(30)", "broken", 1.0)])
+def test_consumer_fork_mode(tmp_path, body, status, timeout):
+    exp = _experiment(tmp_path, body)
+    cons = Consumer(exp, trial_runner="fork", trial_timeout=timeout, heartbeat=0.2)
+    try:
+        trial = exp.reserve_trial(worker="w0")
+        t0 = time.monotonic()
+        assert cons.consume(trial) == status
+        if timeout:
+            assert time.monotonic() - t0 < 20
+        if status == "completed":
+            doc = exp.storage.read("trials", {"_id": trial.id})[0]
+            assert doc["status"] == "completed"
+            # a forked child, not the worker itself
+            assert int(doc["results"][0]["value"]) not in (os.getpid(), cons._forkserver.proc.pid)
+    finally:
+        cons.close()
+
+
+def test_cli_trial_runner_fork(tmp_path):
+    script = tmp_path / "bb.py"
+    script.write_text(textwrap.dedent(f"""
+        import argparse, sys
+        sys.path.insert(0, {ROOT!r})
+        from orion_amd.client import report_results
+        a = argparse.ArgumentParser(); a.add_argument("-x", type=float); x = a.parse_args().x
+        report_results([dict(name="o", type="objective", value=(x - 0.3) ** 2)])
+    """))
+    db = tmp_path / "db.sqlite"
+    env = dict(os.environ, PYTHONPATH=ROOT, METAOPT_DB_TYPE="sqlite", METAOPT_DB_ADDRESS=str(db),
+               METAOPT_DB_NAME="t")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bin", "orion"), "-n", "forkcli", "--max-trials", "4",
+                        "--trial-runner", "fork", str(script), "-x~uniform(0, 1)"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    import sqlite3
+    con = sqlite3.connect(str(db))
+    n = con.execute("select count(*) from trials").fetchone()[0]
+    assert n >= 4
