@@ -77,8 +77,7 @@ def _run_child(argv, env, cwd, fds):
             sys.stdout.flush()
             sys.stderr.flush()
         finally:
-            os._exit(code & 0xFF)
-    del fds  # held open until _exit: the GPU lease's lock descriptors
+            os._exit(code & 0xFF)  # ``fds`` (the lease's lock descriptors) stay open until here
 
 
 def serve(sock: socket.socket, preload=DEFAULT_PRELOAD):
@@ -89,6 +88,7 @@ def serve(sock: socket.socket, preload=DEFAULT_PRELOAD):
             __import__(mod)
         except Exception as exc:  # noqa: BLE001 - a missing optional module only costs speed
             print(f"[orion forkserver] preload {mod} failed: {exc}", file=sys.stderr, flush=True)
+
     # forking a process whose HIP runtime is up is not supported: the preload must not touch
     # the GPU (torch.cuda.is_available() would); refuse to fork if something did
     torch = sys.modules.get("torch")
