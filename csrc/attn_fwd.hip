@@ -183,13 +183,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
         const bool need_mask = (CAUSAL && (k0 + BN - 1 > qwb + off)) || (k0 + BN > p.Tk);
         if (need_mask) {
           // key k0 + kb*32 + rowoff(r) + 4*h32 is visible iff rowoff(r) <= lim
+          // as min(s, (lim - rowoff + 0.5) * 1e35): >= 5e34 where visible (s unchanged), <= -5e34
+          // where not (exp2 of it is 0, and it stays below the running max's -1e30 start) --
+          // one fma + one min per score instead of a compare, the VCC hazard wait and a select
           const int vis = CAUSAL ? min(qwb + l32 + off, p.Tk - 1) : p.Tk - 1;
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) {
-            const int lim = vis - (k0 + kb * 32 + 4 * h32);
+            const float fl = (float)(vis - (k0 + kb * 32 + 4 * h32));
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-              s[qb][kb][r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[qb][kb][r];
+              s[qb][kb][r] = fminf(s[qb][kb][r], fmaf(fl, 1e35f, (0.5f - (float)((r & 3) + 8 * (r >> 2))) * 1e35f));
           }
         }
         // row max: four independent 8-value chains of v_max3, then one combine
