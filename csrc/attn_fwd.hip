@@ -189,10 +189,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
           const int vis = CAUSAL ? min(qwb + l32 + off, p.Tk - 1) : p.Tk - 1;
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) {
-            const float fl = (float)(vis - (k0 + kb * 32 + 4 * h32));
+            if constexpr (CAUSAL && D == 64 && QB == 2) {  // elsewhere the constants cost registers (spills)
+              const float fl = (float)(vis - (k0 + kb * 32 + 4 * h32));
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-              s[qb][kb][r] = fminf(s[qb][kb][r], fmaf(fl, 1e35f, (0.5f - (float)((r & 3) + 8 * (r >> 2))) * 1e35f));
+              for (int r = 0; r < 16; ++r)
+                s[qb][kb][r] = fminf(s[qb][kb][r], fmaf(fl, 1e35f, (0.5f - (float)((r & 3) + 8 * (r >> 2))) * 1e35f));
+            } else {
+              const int lim = vis - (k0 + kb * 32 + 4 * h32);
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                s[qb][kb][r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[qb][kb][r];
+            }
           }
         }
         // row max: four independent 8-value chains of v_max3, then one combine
