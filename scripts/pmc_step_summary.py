@@ -24,8 +24,16 @@ def group(name):
     n = name.lower()
     if "gemm_phased" in n:
         return "GEMM in-tree phased (weight gradients)"
+    if "gemm16_kernel<true, true, 4" in n:
+        return "GEMM gemm16 weight gradients (split-K)"
+    if "gemm16_kernel<false, true, 3" in n:
+        return "GEMM gemm16 dgrad + GELU' + bias-grad epilogue"
+    if "gemm16_kernel<false, false, 2" in n:
+        return "GEMM gemm16 fwd + bias + GELU epilogue"
+    if "gemm16_kernel" in n:
+        return "GEMM gemm16 input gradients"
     if "cijk" in n or "gemm[" in n:
-        return "GEMM hipBLASLt (forward, input gradients)"
+        return "GEMM hipBLASLt (forward)"
     for key, g in (("attn_fwd", "attention forward"), ("attn_bwd_kv", "attention bwd dK/dV"),
                    ("attn_bwd_dq", "attention bwd dQ"), ("attn_delta", "attention delta"),
                    ("ln_fwd", "LayerNorm fwd"), ("ln_bwd", "LayerNorm bwd"),
