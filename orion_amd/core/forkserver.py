@@ -122,9 +122,14 @@ def serve(sock: socket.socket, preload=DEFAULT_PRELOAD):
         buf += data
         while b"\n" in buf:
             line, buf = buf.split(b"\n", 1)
-            req = json.loads(line)
-            if gpu_up:
-                send({"error": "the GPU was initialised in the fork server; not forking"})
+            try:
+                req = json.loads(line)
+                req = dict(argv=list(req["argv"]), env=dict(req["env"]), cwd=str(req["cwd"]))
+            except (ValueError, KeyError, TypeError) as exc:
+                req = None
+                err = f"malformed request: {exc}"
+            if gpu_up or req is None:
+                send({"error": err if req is None else "the GPU was initialised in the fork server; not forking"})
                 for fd in fds:
                     os.close(fd)
                 fds = []

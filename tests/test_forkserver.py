@@ -56,6 +56,20 @@ def test_failures_map_to_exit_codes(server, tmp_path, body, rc):
     assert server.spawn([s], dict(os.environ), cwd=str(tmp_path)).wait(timeout=30) == rc
 
 
+def test_malformed_request_is_refused_and_server_keeps_serving(server, tmp_path):
+    import json
+    import socket
+    with server._spawn_lock:
+        socket.send_fds(server._sock, [b"not json\n" + json.dumps({"argv": ["x"]}).encode() + b"\n"], [])
+        with server._cv:
+            while len(server._replies) < 2:
+                assert server._cv.wait(10.0)
+            replies = [server._replies.pop(0) for _ in range(2)]
+    assert all("malformed request" in r.get("error", "") for r in replies), replies
+    s = _script(tmp_path, "ok.py", "pass")
+    assert server.spawn([s], dict(os.environ), cwd=str(tmp_path)).wait(timeout=30) == 0
+
+
 def test_timeout_and_killpg(server, tmp_path):
     s = _script(tmp_path, "hang.py", """
         import subprocess, sys, time
