@@ -69,3 +69,15 @@ def test_pmc_step_summary_utilisation_and_traffic(tmp_path):
     assert gemm[-3] == "50.0%"
     assert gemm[-2] == f"{2 * 1024 * 600_000 / 1e9:.2f}"
     assert gemm[-1] == "2.05"
+
+
+def test_pmc_step_summary_groups_gemm16_by_epilogue():
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import pmc_step_summary as pss
+    g = pss.group
+    assert g("void orion::gemm16_kernel<true, true, 4, false>(orion::GemmArgs)").endswith("weight gradients (split-K)")
+    assert "GELU' + bias-grad" in g("void orion::gemm16_kernel<false, true, 3, false>(orion::GemmArgs)")
+    assert "bias + GELU" in g("void orion::gemm16_kernel<false, false, 2, false>(orion::GemmArgs)")
+    assert g("void orion::gemm16_kernel<false, true, 0, false>(orion::GemmArgs)") == "GEMM gemm16 input gradients"
+    assert g("Custom_Cijk_Alik_Bljk_BBS_BH_MT256x256x64") == "GEMM hipBLASLt (forward)"
+    assert g("void orion::attn_bwd_kv_kernel<64, true, false>(orion::AttnParams)") == "attention bwd dK/dV"
