@@ -3,7 +3,7 @@
 #   m: MFMA busy cycles, MFMA / VALU instruction counts, GPU-active cycles
 #   f: HBM-side fetch bytes (TCC FETCH_SIZE)      w: write bytes (TCC WRITE_SIZE)
 # over a 2-step GPT-2 bench, then the per-kernel-group table of scripts/pmc_step_summary.py.
-# usage: scripts/pmc_step.sh TAG [bench args]
+# usage: [PMC_PASS_TIMEOUT=seconds] scripts/pmc_step.sh TAG [bench args]
 set -o pipefail
 cd "$(dirname "$0")/.."
 REPO=$(pwd)
@@ -16,7 +16,7 @@ cd /tmp || exit 1
 run() {
   p=$1; shift
   # shellcheck disable=SC2086
-  timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/$p" -o run \
+  timeout -s KILL "${PMC_PASS_TIMEOUT:-150}" rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/$p" -o run \
     -- python3 "$REPO/bench.py" $ARGS > "$OUT/$p.log" 2>&1 || { tail -20 "$OUT/$p.log"; return 1; }
 }
 run m SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE && \

@@ -39,7 +39,9 @@ def group(name):
                    ("ln_fwd", "LayerNorm fwd"), ("ln_bwd", "LayerNorm bwd"),
                    ("bias_gelu_fwd", "bias+GELU fwd"), ("bias_gelu_bwd", "bias+GELU bwd"),
                    ("xent", "cross-entropy"), ("adamw", "AdamW"), ("colsum", "column sums"),
-                   ("slab_sum", "split-K slab sums")):
+                   ("slab_sum", "split-K slab sums"), ("rms_fwd", "RMSNorm fwd"), ("rms_bwd", "RMSNorm bwd"),
+                   ("swiglu_fwd", "SwiGLU fwd"), ("swiglu_bwd", "SwiGLU bwd"), ("rope", "RoPE"),
+                   ("sumsq", "gradient norm")):
         if key in n:
             return g
     return "other"
