@@ -49,14 +49,27 @@ from .trial import Trial
 log = logging.getLogger(__name__)
 
 
+# prctl resolved once, in the parent, at import: the preexec_fn below runs in the child
+# between fork and exec, where importing a module or dlopen-ing a library can deadlock on a
+# lock another thread of the worker held at fork time (pymongo's monitor threads, the fork
+# server's reader thread) -- so the child only makes the call
+try:
+    import ctypes as _ctypes
+    _PRCTL = _ctypes.CDLL(None, use_errno=True).prctl
+    _PRCTL.restype = _ctypes.c_int
+except (OSError, AttributeError):  # pragma: no cover - no libc prctl (non-Linux)
+    _PRCTL = None
+_PR_SET_PDEATHSIG = 1
+_SIGTERM = int(signal.SIGTERM)
+
+
 def _term_with_parent(parent_pid):
     """preexec_fn of a trial process: SIGTERM when the worker dies (any way it dies)."""
+    prctl = _PRCTL
+
     def arm():
-        try:
-            import ctypes
-            ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
-        except OSError:
-            pass
+        if prctl is not None:
+            prctl(_PR_SET_PDEATHSIG, _SIGTERM, 0, 0, 0)
         if os.getppid() != parent_pid:
             os._exit(1)
     return arm

@@ -149,6 +149,78 @@ class Experiment:
             log.debug("lost the reservation race for %s; retrying", sel.id)
         return None
 
+    # ------------------------------------------------------------------ trial budget
+    # Trials that count toward ``max_trials``: every status but ``broken``.  The experiment
+    # document carries ``budget = {"used": n, "t": time of the last change}``, the number of
+    # such trials registered or about to be; a producer takes tokens with a compare-and-swap
+    # on it BEFORE inserting trials, a broken trial gives its token back, so concurrent
+    # producers can never register more than ``max_trials`` counting trials (the reference
+    # counted, then inserted: W workers overshot by up to W x pool_size,
+    # src/orion/core/worker/producer.py:35-45).
+    LIVE_STATI = ("new", "reserved", "suspended", "interrupted", "completed")
+    BUDGET_ATTEMPTS = 256
+
+    def _budgeted(self):
+        return self.max_trials not in (None, float("inf")) and self._id is not None
+
+    def _budget_doc(self):
+        docs = self._db.read("experiments", {"_id": self._id}, selection={"budget": 1})
+        return docs[0].get("budget") if docs else None
+
+    def _budget_cas(self, old, used):
+        q = {"_id": self._id}
+        if old is None:
+            q["budget"] = {"$exists": False}
+        else:
+            q["budget.used"], q["budget.t"] = old["used"], old["t"]
+        return self._db.read_and_write("experiments", q, {"budget": {"used": int(used), "t": utcnow()}}) is not None
+
+    def claim_budget(self, n):
+        """Take up to ``n`` registration tokens; returns how many were taken (0 when the budget
+        is spent).  Unbudgeted experiments (``max_trials`` infinite) always get ``n``."""
+        if n <= 0:
+            return 0
+        if not self._budgeted():
+            return n
+        for _ in range(self.BUDGET_ATTEMPTS):
+            b = self._budget_doc()
+            if b is None:  # first use (or an experiment from before the counter): seed it
+                self._budget_cas(None, self.count_trials(self.LIVE_STATI))
+                continue
+            k = min(n, int(self.max_trials) - int(b["used"]))
+            if k <= 0:
+                return 0
+            if self._budget_cas(b, int(b["used"]) + k):
+                return k
+        log.warning("trial budget: no token after %d attempts (heavy contention)", self.BUDGET_ATTEMPTS)
+        return 0
+
+    def release_budget(self, k):
+        """Give back ``k`` tokens (a suggestion shortfall, a failed insert, a broken trial)."""
+        if k <= 0 or not self._budgeted():
+            return
+        for _ in range(self.BUDGET_ATTEMPTS):
+            b = self._budget_doc()
+            if b is None:
+                return
+            if self._budget_cas(b, max(0, int(b["used"]) - k)):
+                return
+
+    def reconcile_budget(self, grace_s=60.0):
+        """A producer that died between taking tokens and inserting its trials leaks them:
+        when the counter has not moved for ``grace_s`` and exceeds the counting trials that
+        exist, set it back to that count.  Returns the number of tokens recovered."""
+        if not self._budgeted():
+            return 0
+        b = self._budget_doc()
+        if b is None or utcnow() - b["t"] < datetime.timedelta(seconds=grace_s):
+            return 0
+        live = self.count_trials(self.LIVE_STATI)
+        if live < int(b["used"]) and self._budget_cas(b, live):
+            log.warning("trial budget: recovered %d token(s) leaked by a dead producer", int(b["used"]) - live)
+            return int(b["used"]) - live
+        return 0
+
     def register_trials(self, trials):
         stamp = utcnow()
         for t in trials:
@@ -191,11 +263,16 @@ class Experiment:
         """Move ``trial`` to ``status``; with ``only_if`` it is a CAS on the current status
         (and on the reserving worker, see :meth:`_owned`)."""
         q = {"_id": trial.id} if only_if is None else self._owned(trial, only_if)
+        if status == "broken":  # only a trial that still counted gives a token back
+            q.setdefault("status", {"$in": list(self.LIVE_STATI)})
         trial.status = status
         upd = {"status": status}
         if status in ("broken", "completed"):
             upd["end_time"] = trial.end_time = utcnow()
-        return self._db.read_and_write("trials", q, upd) is not None
+        ok = self._db.read_and_write("trials", q, upd) is not None
+        if ok and status == "broken":
+            self.release_budget(1)
+        return ok
 
     def record_lease(self, trial, gpu_ids):
         """The trial got its GPUs and starts executing: record the device ids and move

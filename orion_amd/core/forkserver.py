@@ -74,10 +74,26 @@ def _run_child(argv, env, cwd, fds):
             code = 1
     finally:
         try:
+            _interpreter_shutdown()
             sys.stdout.flush()
             sys.stderr.flush()
         finally:
             os._exit(code & 0xFF)  # ``fds`` (the lease's lock descriptors) stay open until here
+
+
+def _interpreter_shutdown():
+    """What a normal interpreter exit does before the process ends, which ``os._exit`` alone
+    skips: join the non-daemon threads the script started, then run the ``atexit`` handlers
+    (logging.shutdown, result writers, tracker flushes) -- so a forked trial keeps the
+    ``Popen`` contract of an exec'd one."""
+    import atexit
+    import threading
+    try:
+        threading._shutdown()  # the interpreter's own join of non-daemon threads
+    except BaseException:  # noqa: BLE001 - a failing thread join must not skip the atexit handlers
+        import traceback
+        traceback.print_exc()
+    atexit._run_exitfuncs()  # prints (does not raise) a handler's exception, as at exit
 
 
 def serve(sock: socket.socket, preload=DEFAULT_PRELOAD):
@@ -112,13 +128,19 @@ def serve(sock: socket.socket, preload=DEFAULT_PRELOAD):
 
     import select
     buf = b""
+    fds: list = []  # descriptors received since the last complete request line
     while True:
         reap()
         if not select.select([sock], [], [], 0.05)[0]:
             continue
-        data, fds, _, _ = socket.recv_fds(sock, 1 << 16, 16)
+        data, new_fds, _, _ = socket.recv_fds(sock, 1 << 16, 16)
         if not data:
+            for fd in fds + list(new_fds):
+                os.close(fd)
             break  # the worker closed the socket (or died): children get SIGTERM via PDEATHSIG
+        # a request longer than one recv (a big environment) brings its descriptors with its
+        # FIRST chunk: keep them until the newline that completes the request arrives
+        fds += list(new_fds)
         buf += data
         while b"\n" in buf:
             line, buf = buf.split(b"\n", 1)

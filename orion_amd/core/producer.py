@@ -27,8 +27,9 @@ class Producer:
         self.num_new_trials = experiment.pool_size
 
     def budget(self):
-        """How many more trials may be registered: ``pool_size``, capped by what is left of
-        ``max_trials`` after the registered non-broken trials."""
+        """How many more trials may be registered (a read-only estimate): ``pool_size``, capped
+        by what is left of ``max_trials`` after the registered non-broken trials.  ``produce``
+        takes its tokens atomically (``Experiment.claim_budget``)."""
         max_trials = getattr(self.experiment, "max_trials", float("inf"))
         n = self.num_new_trials
         if max_trials is not None and max_trials != float("inf"):
@@ -38,14 +39,24 @@ class Producer:
         return max(0, n)
 
     def produce(self):
-        n = self.budget()
+        """Register up to ``pool_size`` suggestions, never past ``max_trials``: the tokens are
+        taken with a compare-and-swap on the experiment's budget counter before the insert,
+        and whatever is not inserted is given back."""
+        claim = getattr(self.experiment, "claim_budget", None)
+        n = claim(self.num_new_trials) if claim else self.budget()
         if n <= 0:
             return 0
-        points = self.algorithm.suggest(n)
-        trials = [format_trials.tuple_to_trial(p, self.space) for p in points]
-        log.debug("registering %d new trial(s)", len(trials))
-        self.experiment.register_trials(trials)
-        return len(trials)
+        inserted = 0
+        try:
+            points = self.algorithm.suggest(n) or []
+            trials = [format_trials.tuple_to_trial(p, self.space) for p in points[:n]]
+            log.debug("registering %d new trial(s)", len(trials))
+            self.experiment.register_trials(trials)
+            inserted = len(trials)
+        finally:
+            if claim and inserted < n:
+                self.experiment.release_budget(n - inserted)
+        return inserted
 
     def update(self):
         trials = self.experiment.fetch_completed_trials()

@@ -59,6 +59,7 @@ def _workon(experiment, consumer, max_broken, idle_sleep):
             if experiment.finish_if_done():
                 break
             experiment.fix_lost_trials(stale_after)
+            experiment.reconcile_budget()
             if (experiment.count_trials(("new", "suspended", "interrupted")) == 0
                     and producer.produce() > 0):
                 sleep = idle_sleep[0]

@@ -24,6 +24,11 @@ def ext_available() -> bool:
     return _loaded or os.path.isfile(EXT_PATH)
 
 
+def ext_loaded() -> bool:
+    """True once ``_C.so`` has been loaded into this process."""
+    return _loaded
+
+
 def load_ext(required: bool = False) -> bool:
     """Load ``_C.so`` once.  With ``required=True`` a missing build raises."""
     global _loaded

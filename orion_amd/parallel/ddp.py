@@ -371,6 +371,22 @@ class ShardedGradReducer(GradBucketReducer):
             dist.all_gather_into_tensor(full[b0:b1], shard[so:so + ln].contiguous(), group=self.group)
         return full
 
+    def gather_full_host(self, shard: torch.Tensor, keep: bool) -> torch.Tensor | None:
+        """The arena-layout tensor of ``gather_full`` in HOST memory, only where ``keep``
+        (the checkpoint writer): every rank joins the per-bucket all-gathers through one
+        bucket-sized device buffer, the others drop each bucket at once, so a non-writing rank
+        never holds the full tensor on the device or the host (Llama-7B: 27 GB per moment)."""
+        full = torch.zeros(self.arena.numel, dtype=shard.dtype) if keep else None
+        tmp = None
+        for bi, _, so, ln in self.shard_ranges:
+            b0, b1, _ = self.buckets[bi]
+            if tmp is None or tmp.numel() < b1 - b0:
+                tmp = torch.empty(b1 - b0, dtype=shard.dtype, device=shard.device)
+            dist.all_gather_into_tensor(tmp[:b1 - b0], shard[so:so + ln].contiguous(), group=self.group)
+            if keep:
+                full[b0:b1].copy_(tmp[:b1 - b0])
+        return full
+
     def _launch(self, bi):
         if self._handles[bi] is not None:
             return

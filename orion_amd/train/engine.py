@@ -210,6 +210,20 @@ class Trainer:
         self.iter_num += 1
         return self._static_loss
 
+    def check_token_ids(self):
+        """Raise IndexError if an embedding kernel saw a token id outside the table since the
+        last check (the kernels clamp / skip such ids and raise a device flag rather than
+        fault; ops/embedding.py).  Synchronises: call it where the loop syncs anyway (log and
+        eval intervals)."""
+        dev = next(self.model.parameters()).device
+        if dev.type != "cuda":
+            return
+        from ..ops import embedding
+        from ..ops._ext import ext_loaded
+        if ext_loaded() and embedding.id_error(dev):
+            raise IndexError("token id out of range for the embedding table (device flag set by the "
+                             "embedding kernels; the batch was trained with those ids clamped)")
+
     def full_master(self):
         """fp32 master weights in arena layout (gathered from the shards under ZeRO-1)."""
         return self.reducer.gather_full(self.opt.master) if self.zero1 else self.opt.master

@@ -160,3 +160,44 @@ def test_cli_trial_runner_fork(tmp_path):
     con = sqlite3.connect(str(db))
     n = con.execute("select count(*) from trials").fetchone()[0]
     assert n >= 4
+
+
+def test_non_daemon_threads_and_atexit_run_before_exit(server, tmp_path):
+    """A forked trial ends like an interpreter: its non-daemon threads are joined and its
+    atexit handlers run before the exit status is reported."""
+    out = tmp_path / "late.txt"
+    s = _script(tmp_path, "t.py", f"""
+        import atexit, threading, time
+        def late():
+            time.sleep(0.3)
+            with open({str(out)!r}, "a") as f:
+                f.write("thread;")
+        threading.Thread(target=late).start()
+        atexit.register(lambda: open({str(out)!r}, "a").write("atexit;"))
+    """)
+    assert server.spawn([s], dict(os.environ), cwd=str(tmp_path)).wait(timeout=30) == 0
+    assert out.read_text() == "thread;atexit;"
+
+
+def test_request_larger_than_one_recv_keeps_its_descriptors(server, tmp_path):
+    """A request whose JSON line spans several recv calls (an environment over 64 KiB) still
+    hands the lease descriptors, sent with its first chunk, to the forked child (it holds a
+    descriptor of the same pipe: descriptor numbers differ across SCM_RIGHTS)."""
+    r, w = os.pipe()
+    out = tmp_path / "fds.txt"
+    s = _script(tmp_path, "fd.py", f"""
+        import os
+        links = []
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                links.append(os.readlink("/proc/self/fd/" + fd))
+            except OSError:
+                pass
+        open({str(out)!r}, "w").write(str(os.environ["PIPE"] in links))
+    """)
+    env = dict(os.environ, BIG="x" * 200_000, PIPE=os.readlink(f"/proc/self/fd/{w}"))
+    p = server.spawn([s], env, cwd=str(tmp_path), pass_fds=(w,))
+    os.close(w)
+    os.close(r)
+    assert p.wait(timeout=30) == 0
+    assert out.read_text() == "True"

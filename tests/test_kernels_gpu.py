@@ -718,3 +718,23 @@ def test_embedding_rejects_out_of_range_ids():
     want = torch.zeros(V, Cc, device=DEV).index_add_(0, good[ok], dx.float()[ok])
     assert torch.equal(table, want)
     assert float(guard.abs().max()) == 0.0
+
+
+def test_trainer_check_token_ids_raises_after_bad_batch():
+    """Out-of-range ids past the first (host-checked) call train with clamped ids and set the
+    device flag; Trainer.check_token_ids -- called by train.py at every log interval -- turns
+    the flag into an IndexError (the flag used to be read by nothing)."""
+    from orion_amd.models.gpt2 import build_gpt2
+    from orion_amd.train.engine import Trainer
+    torch.manual_seed(0)
+    model = build_gpt2("gpt2-tiny", block_size=32).to(DEV)
+    tr = Trainer(model)
+    V = model.config.vocab_size
+    x = torch.randint(0, V, (2, 32), device=DEV)
+    tr.step([(x, x)])
+    tr.check_token_ids()  # clean data: no error
+    bad = x.clone()
+    bad[0, 3] = V + 5
+    tr.step([(bad, x)])
+    with pytest.raises(IndexError):
+        tr.check_token_ids()

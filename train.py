@@ -209,6 +209,8 @@ def main(argv=None):
         loss = trainer.step(batches)
         if prof is not None:
             prof.step()
+        if it % cfg["log_interval"] == 0:
+            trainer.check_token_ids()  # raises on out-of-range token data (one sync per log)
         if it % cfg["log_interval"] == 0 and master:
             lossf = float(loss)
             dt = time.time() - t0
