@@ -71,10 +71,12 @@ def parse():
                     help="gradient arena dtype (fp32: accumulation and all-reduce in fp32)")
     ap.add_argument("--hip-graph", action="store_true",
                     help="capture the whole training step in a HIP graph (single GPU)")
-    ap.add_argument("--zero1", action="store_true",
+    ap.add_argument("--zero1", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
                     help="ZeRO-1: reduce-scatter gradients, AdamW on this rank's 1/N shard of the "
-                         "fp32 master / Adam state, all-gather the bf16 weights (with one GPU: a "
-                         "world-1 rehearsal of the sharded path)")
+                         "fp32 master / Adam state, all-gather the bf16 weights (overlapped with the "
+                         "next forward).  auto (default): on for models of >= 1B parameters at "
+                         "N > 1 GPUs; a bare --zero1 = on (with one GPU: a world-1 rehearsal of "
+                         "the sharded path)")
     return ap.parse_args()
 
 
@@ -94,7 +96,7 @@ def main():
         dev = launch.device_for(local_rank, local_world, args.dist_backend)
         torch.cuda.set_device(dev)
     rccl_log = None
-    if world == 1 and args.zero1:
+    if world == 1 and args.zero1 == "on":
         # a one-rank process group so the sharded optimizer path runs as it would at N > 1
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(launch.free_port()))
@@ -145,7 +147,7 @@ def main():
     if args.impl == "native":
         trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb, graph=args.hip_graph and world == 1,
                           grad_dtype=torch.float32 if args.grad_dtype == "fp32" else torch.bfloat16,
-                          ddp_timing=world > 1, zero1=args.zero1)
+                          ddp_timing=world > 1, zero1={"auto": None, "on": True, "off": False}[args.zero1])
         step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
     else:
         ddp_model = model
@@ -251,8 +253,9 @@ def main():
             "loss": round(final_loss, 4),
             "max_mem_gb": (round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
                            if dev.type == "cuda" else None),
-            "dist_backend": args.dist_backend if world > 1 or args.zero1 else None,
+            "dist_backend": args.dist_backend if world > 1 or args.zero1 == "on" else None,
             "zero1": bool(args.impl == "native" and trainer.zero1),
+            "zero1_mode": args.zero1,
             "optimizer_state_gb_per_rank": (round(3 * 4 * trainer.opt.master.numel() / 2**30, 2)
                                             if args.impl == "native" else None),
             "allreduce_busbw_gbps": busbw,

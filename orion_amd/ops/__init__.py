@@ -270,3 +270,52 @@ __all__ = [
     "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy",
     "linear_cross_entropy",
 ]
+
+
+# ------------------------------------------------------------------ parameter-read guards
+# ZeRO-1 leaves the weight all-gathers of the previous optimizer step in flight
+# (parallel/ddp.py ShardedGradReducer.gather_params).  The fused ops read weights of several
+# modules at once from the model's top-level forward (block i's add+LayerNorm takes block
+# i+1's ln_1, the embedding takes block 0's), so module forward hooks alone cannot say when a
+# weight is first read: every op here that takes weights first hands its arguments to the
+# registered guards, which wait for the gathers of the buckets those tensors live in.
+_PARAM_GUARDS: list = []
+
+
+def add_param_guard(fn):
+    """Register ``fn(tensors)`` to run before any weight-taking op; returns a remover.  A
+    bound method is held weakly (a dropped reducer unregisters itself)."""
+    import weakref
+    ref_ = weakref.WeakMethod(fn) if hasattr(fn, "__self__") else (lambda: fn)
+    _PARAM_GUARDS.append(ref_)
+
+    def remove():
+        if ref_ in _PARAM_GUARDS:
+            _PARAM_GUARDS.remove(ref_)
+    return remove
+
+
+def _guarded(fn):
+    import functools
+
+    @functools.wraps(fn)
+    def run(*args, **kw):
+        if _PARAM_GUARDS:
+            ts = [a for a in args if isinstance(a, torch.Tensor)]
+            ts += [a for a in kw.values() if isinstance(a, torch.Tensor)]
+            for g in list(_PARAM_GUARDS):
+                f = g()
+                if f is None:
+                    _PARAM_GUARDS.remove(g)
+                else:
+                    f(ts)
+        return fn(*args, **kw)
+    run.__wrapped_op__ = fn
+    return run
+
+
+for _name in ("layer_norm", "add_layer_norm", "add_rms_norm", "linear", "rms_norm", "bias_gelu",
+              "gelu_linear", "mlp", "embed_layer_norm", "add_broadcast", "linear_attention_qkv",
+              "linear_cross_entropy"):
+    globals()[_name] = _guarded(globals()[_name])
+del _name

@@ -37,6 +37,9 @@ class OptimConfig:
 _GRAPH_SYNC = os.environ.get("ORION_GRAPH_SYNC") == "1"  # debugging aid
 
 
+ZERO1_AUTO_PARAMS = int(float(os.environ.get("ORION_ZERO1_AUTO_PARAMS", "1e9")))
+
+
 def cosine_lr(it: int, cfg: OptimConfig) -> float:
     """nanoGPT's schedule: linear warmup, cosine decay to min_lr."""
     if not cfg.decay_lr:
@@ -70,7 +73,7 @@ class Trainer:
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float | None = None, arena_dtype=None,
                  graph: bool = False, grad_dtype=None, ddp_timing: bool = False,
-                 zero1: bool = False):
+                 zero1: bool | None = None):
         self.model = model
         self.cfg = optim or OptimConfig()
         dev = next(model.parameters()).device
@@ -86,7 +89,14 @@ class Trainer:
         # ZeRO-1 (parallel/ddp.py ShardedGradReducer): reduce-scatter the gradient buckets, AdamW
         # on this rank's 1/N shard of master / m / v, all-gather the bf16 weights.  Also valid
         # with one rank (a rehearsal of the sharded code path).
-        self.zero1 = bool(zero1) and dist.is_available() and dist.is_initialized()
+        # zero1=None (auto): sharded from ZERO1_AUTO_PARAMS parameters up when there is more
+        # than one rank -- a 7B model's replicated fp32 master + Adam state is 81 GB per GPU and
+        # its all-reduce moves 2 (N-1)/N x 27 GB of fp32 gradients per step
+        dist_on = dist.is_available() and dist.is_initialized()
+        if zero1 is None:
+            zero1 = (dist_on and dist.get_world_size() > 1
+                     and sum(p.numel() for p in model.parameters()) >= ZERO1_AUTO_PARAMS)
+        self.zero1 = bool(zero1) and dist_on
         self.reducer = None
         if self.zero1:
             from ..parallel.ddp import ShardedGradReducer, zero1_pad_names
@@ -98,6 +108,7 @@ class Trainer:
             with torch.no_grad():
                 self.arena.params.copy_(self.arena.init_fp32)
             self.reducer = ShardedGradReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing)
+            self.reducer.install_gather_hooks(model)
             self.reducer.init_fp32 = self.reducer.shard_of(self.arena.init_fp32)
             self.arena.init_fp32 = None
             self.opt = FlatAdamW(self.reducer, lr=self.cfg.learning_rate,
@@ -209,6 +220,12 @@ class Trainer:
         self.opt.step_count += 1
         self.iter_num += 1
         return self._static_loss
+
+    def sync_params(self):
+        """Wait for ZeRO-1's overlapped weight all-gathers (a no-op otherwise): for code that
+        reads ``arena.params`` directly instead of through a module forward."""
+        if self.zero1:
+            self.reducer.wait_params()
 
     def check_token_ids(self):
         """Raise IndexError if an embedding kernel saw a token id outside the table since the

@@ -55,6 +55,7 @@ def _worker(rank, world, port, bucket_mb, clip, ckdir, out):
     full_ref = res[False][1].state_dict_fp32(res[False][0])
     full_z = res[True][1].state_dict_fp32(res[True][0])
     tz = res[True][2]
+    tz.sync_params()
     shard_numel = tz.reducer.shard_numel
     # bf16-free CPU arena: the compute weights are the gathered master
     params_match = all(torch.equal(tz.arena.params[s.offset:s.offset + s.numel],
@@ -135,3 +136,45 @@ def test_zero1_world_one_rehearsal():
             assert torch.allclose(sa[k], sb[k], rtol=1e-6, atol=1e-7), k
     finally:
         dist.destroy_process_group()
+
+
+def _overlap_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    from orion_amd.parallel.launch import init_process_group
+    init_process_group("gloo")
+    g = torch.Generator().manual_seed(7)
+    data = [(torch.randint(0, 50257, (2, 32), generator=g), torch.randint(0, 50257, (2, 32), generator=g))
+            for _ in range(3 * world)]
+    got = []
+    for overlap in (False, True):
+        tr = _trainer(True, 0.05)
+        tr.reducer.overlap_gather = overlap
+        for step in range(3):
+            tr.step([data[step * world + rank]])
+            if overlap:  # the gathers are still in flight when step() returns
+                assert any(h is not None for h in tr.reducer._pgather)
+        tr.sync_params()
+        got.append((tr.arena.params.clone(), tr.opt.master.clone()))
+    out.put((rank, torch.equal(got[0][0], got[1][0]), torch.equal(got[0][1], got[1][1]),
+             len(tr.reducer._hooks)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_zero1_overlapped_gather_matches_serial(world):
+    """ZeRO-1 weight all-gathers left in flight after the step and waited for per bucket by
+    forward pre-hooks give weights bit-identical to gathering them all
+    before the next forward, after 3 steps on 2 and 4 gloo ranks."""
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, same_params, same_master, nhooks in res:
+        assert same_params and same_master, rank
+        assert nhooks > 0

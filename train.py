@@ -43,7 +43,7 @@ DEFAULTS = dict(
     backend="nccl", device="cuda", dtype="bfloat16", seed=1337, bucket_mb=0.0,
     # zero1: shard the fp32 master / Adam state over the data-parallel ranks (ZeRO-1:
     # reduce-scatter gradients, all-gather weights; parallel/ddp.py ShardedGradReducer)
-    zero1=False,
+    zero1=None,  # None: auto (sharded optimizer from 1B parameters at more than one rank)
     data_root="data",
     # tracing: profile_steps > 0 records that many steps, starting at
     # profile_start, with torch.profiler and writes a Chrome trace to out_dir
@@ -142,7 +142,7 @@ def main(argv=None):
                        warmup_iters=cfg["warmup_iters"], lr_decay_iters=cfg["lr_decay_iters"],
                        min_lr=cfg["min_lr"], decay_lr=cfg["decay_lr"])
     trainer = Trainer(model, ocfg, ddp=ddp and world > 1, bucket_mb=cfg["bucket_mb"],
-                      zero1=bool(cfg["zero1"]) and ddp)
+                      zero1=None if cfg["zero1"] is None else bool(cfg["zero1"]) and ddp)
     best_val = 1e9
     if ckpt is not None:
         restore_trainer(trainer, ckpt)
