@@ -1,4 +1,8 @@
-// Flash attention forward + backward for gfx950 (K1/K2 in SURVEY.md §2.11).
+// Flash attention forward + backward for gfx950 (K1/K2 in SURVEY.md §2.11): the round-1/2
+// kernels, now the FALLBACKS -- the forward for offsets past 2 GB (attn_fwd.hip addresses 32-bit
+// buffer offsets), the fused backward (fp32-atomic dQ) for shapes attn_bwd_split.hip cannot
+// address, and the A/B form of the split backward (attn_bwd flags 8).  Round 4 removed the
+// 256-key fused backward (v2) that no default path selected.
 //
 // bf16 in/out, fp32 accumulation, online softmax in base 2, causal or full,
 // GQA (Hq a multiple of Hkv), head dim D in {64, 128}.  Q/K/V/O are addressed
@@ -512,299 +516,6 @@ __global__ __launch_bounds__(bwd_waves<D>() * 64, (D == 64 ? 2 : 1)) void attn_b
   }
 }
 
-// ============================================================================ backward v2
-// 256 keys per workgroup, 8 waves x 32 keys, one workgroup per CU (two waves per SIMD).
-// Compared with the 128-key kernel above it halves the dQ atomic bytes per FLOP (the
-// float-atomic rate, ~1.3 TB/s chip-wide, floors the 128-key form at ~0.42 PF/s at
-// D = 64) and drops the fp32 dQ fold through LDS: every wave writes the dS^T rows of its
-// 32 keys into ONE shared [256 key][BMQ q] LDS image, and after the slice barrier each
-// wave computes two 16 x 16 tiles of the slice's dQ over all 256 keys
-// (v_mfma_f32_16x16x32_bf16, both operands by transposed LDS reads: dS from that image,
-// K from the K image) and adds them with 8 float-atomic instructions.
-//
-// A q slice holds BMQ = 64 rows (two 32-row q blocks).  Per wave and slice: 2 x {S, dP,
-// dV^T, dK^T} (32 v_mfma_f32_32x32x16_bf16) + 16 16x16x32 MFMAs for dQ.  K and V fragments
-// of the wave's keys live in registers (B operands of S and dP).
-// LDS at D = 64: K image 32 KB + Q, dO slices (double-buffered) 32 KB + dS^T image
-// (double-buffered) 64 KB = 128 KB.  One barrier per slice (buffer reuse: loop comment).
-// A 4-wave x 64-key form (one wave per SIMD) measured 1.07 ms vs 0.89 ms for the
-// 128-key kernel at B 64, T 1024, H 12, D 64 (latency-bound: 1.00 ms without atomics);
-// at D = 128 a 256-key form needs more than 512 registers, so D = 128 keeps v1.
-constexpr int BWD2_NW = 8;
-template <int D>
-__host__ __device__ constexpr int bwd2_bmq() { return D == 64 ? 64 : 32; }
-
-// 8-byte-chunk (4 q) swizzle of the dS^T image rows (BMQ q per row): conflict-free
-// ds_write_b64 of 16 consecutive keys, and conflict-free transposed reads of 4 rows at
-// 8-row spacing x 4 chunks per 16-lane group, per half-wave.  128-byte rows (BMQ 64): a
-// bit permutation of k&15; 64-byte rows (BMQ 32): (k>>1)&7.
-template <int BMQ>
-ORION_DEVICE int st_sw(int k) {
-  if constexpr (BMQ == 64) {
-    return (k & 1) | (((k >> 2) & 1) << 1) | (((k >> 3) & 1) << 2) | (((k >> 1) & 1) << 3);
-  } else {
-    return (k >> 1) & 7;
-  }
-}
-// element offset of (key row k, q) in the [256][BMQ] dS^T image
-template <int BMQ>
-ORION_DEVICE int st_off(int k, int q) {
-  return k * BMQ + 4 * ((q >> 2) ^ st_sw<BMQ>(k)) + (q & 3);
-}
-
-ORION_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a),
-                                                 __builtin_bit_cast(bf16x8_mfma, b), c, 0, 0, 0);
-}
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(BWD2_NW * 64, 1) void attn_bwd2_kernel(AttnParams p) {
-  constexpr int NW = BWD2_NW, NT = NW * 64, BNK = 256, BMQ = bwd2_bmq<D>(), QB = BMQ / 32;
-  constexpr int NDB = D / 32, NCH = D / 8;
-  constexpr int KT = BNK * D;     // K image elements
-  constexpr int QT = BMQ * D;     // Q / dO slice elements
-  constexpr int STT = BNK * BMQ;  // dS^T image elements
-  constexpr int NQC = BMQ * NCH;  // 16-byte chunks per Q (or dO) slice
-  constexpr int NSTQ = 2 * NQC / NT;
-  constexpr int D16 = D / 16;                       // 16-wide d blocks of dQ
-  constexpr bool KREG = CAUSAL && D == 64;          // K fragments in registers
-  constexpr int TPW = (BMQ / 16) * D16 / NW;        // 16x16 dQ tiles per wave
-  static_assert(BNK == NW * 32, "one 32-key block per wave");
-  static_assert(TPW >= 1 && TPW * NW == (BMQ / 16) * D16, "dQ tiles must divide over the waves");
-  static_assert(NSTQ % 2 == 0 && NSTQ * NT == 2 * NQC, "Q/dO staging must divide over the threads");
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* Ks = smem;                 // [256][D]
-  bf16_t* Qs = Ks + KT;              // [2][BMQ][D]
-  bf16_t* Ds = Qs + 2 * QT;          // [2][BMQ][D]
-  bf16_t* St = Ds + 2 * QT;          // [2][256][BMQ]
-  float* lse_s = reinterpret_cast<float*>(St + 2 * STT);  // [2][BMQ]
-  float* del_s = lse_s + 2 * BMQ;                          // [2][BMQ]
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int h32 = lane >> 5, l32 = lane & 31;
-  const int BHk = p.B * p.Hkv;
-  const int kt = blockIdx.x / BHk;  // small kt = most work under the causal mask: first
-  const int bh = blockIdx.x % BHk;
-  const int b = bh / p.Hkv, hk = bh % p.Hkv;
-  const int rep = p.Hq / p.Hkv;
-  const int kt0 = kt * BNK, kw0 = kt0 + wv * 32;
-  const int mykey = kw0 + l32;
-  const int off = p.Tk - p.T;
-  const float c = p.scale_log2, inv_c = 1.f / p.scale_log2;
-
-  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
-
-  // K and V fragments of this wave's 32 keys (B operands of S and dP), kept in registers
-  bf16x8 kf[D / 16], vf[D / 16];
-  {
-    const long key = min(mykey, p.Tk - 1);
-#pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      if (KREG) kf[ks] = *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ks * 16 + 8 * h32);
-      vf[ks] = *reinterpret_cast<const bf16x8*>(Vb + key * p.v_st + ks * 16 + 8 * h32);
-    }
-  }
-  // K image: row reads (B operand of S) and transposed reads (B operand of dQ)
-  for (int cidx = tid; cidx < BNK * NCH; cidx += NT) {
-    const int row = cidx / NCH, ch = cidx % NCH;
-    const long key = min(kt0 + row, p.Tk - 1);
-    *reinterpret_cast<bf16x8*>(Ks + loff<D>(row, ch * 8)) =
-        *reinterpret_cast<const bf16x8*>(Kb + key * p.k_st + ch * 8);
-  }
-
-  f32x16 dka[NDB], dva[NDB];
-#pragma unroll
-  for (int db = 0; db < NDB; ++db) { dka[db] = zero16(); dva[db] = zero16(); }
-
-  const int qlo = CAUSAL ? max(0, kt0 - off) : 0;  // first query row that sees any key here
-  const int qi0 = qlo / BMQ;
-  const int nqi = (p.T + BMQ - 1) / BMQ;
-  const int iters_per_head = nqi - qi0;
-  const int total = iters_per_head * rep;
-
-  bf16x8 qdst[NSTQ];
-  float lse_r = 0.f, del_r = 0.f;
-  auto gload = [&](int it) {
-    const int hq = hk * rep + it / iters_per_head;
-    const int qbase = (qi0 + it % iters_per_head) * BMQ;
-    const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
-    const bf16_t* Db = p.dout + b * p.do_sb + hq * p.do_sh;
-#pragma unroll
-    for (int i = 0; i < NSTQ / 2; ++i) {
-      const int cc = tid + i * NT, row = cc / NCH, ch = cc % NCH;
-      const long q = min(qbase + row, p.T - 1);
-      qdst[i] = *reinterpret_cast<const bf16x8*>(Qb + q * p.q_st + ch * 8);
-      qdst[NSTQ / 2 + i] = *reinterpret_cast<const bf16x8*>(Db + q * p.do_st + ch * 8);
-    }
-    if (tid < BMQ) {
-      const long q = min(qbase + tid, p.T - 1);
-      const long r = ((long)b * p.Hq + hq) * p.T + q;
-      lse_r = p.lse[r];
-      del_r = p.delta[r];
-    }
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NSTQ / 2; ++i) {
-      const int cc = tid + i * NT, o = loff<D>(cc / NCH, (cc % NCH) * 8);
-      *reinterpret_cast<bf16x8*>(Qs + buf * QT + o) = qdst[i];
-      *reinterpret_cast<bf16x8*>(Ds + buf * QT + o) = qdst[NSTQ / 2 + i];
-    }
-    if (tid < BMQ) {  // row constants as the initial S / dP accumulators (see the loop)
-      lse_s[buf * BMQ + tid] = -lse_r * inv_c;
-      del_s[buf * BMQ + tid] = -del_r;
-    }
-  };
-
-  // this wave's dQ tiles: d cols 16 d16w.., q rows 16 (qgw TPW + t)..
-  const int d16w = wv % D16, qgw = wv / D16;
-
-  if (total > 0) {
-    gload(0);
-    swrite(0);
-  }
-  __syncthreads();
-  // Buffer reuse with one barrier per slice: slice it reads Q/dO[buf] and writes St[buf]
-  // before the barrier, and reads St[buf] (dQ) after it.  The next writes of Q/dO[buf]
-  // (swrite of slice it+1) and of St[buf] (slice it+2) both come after a later barrier
-  // that every wave reaches only once it is done reading them.
-  // The slice body is instantiated for buffer 0 and 1 (loop unrolled by two), so every LDS
-  // address is a lane-constant base plus an immediate offset.
-  auto slice = [&](const int it, auto bufc) {
-    constexpr int buf = decltype(bufc)::value;
-    const int hq = hk * rep + it / iters_per_head;
-    const int qbase = (qi0 + it % iters_per_head) * BMQ;
-    if (it + 1 < total) gload(it + 1);
-    const bf16_t* Qc = Qs + buf * QT;
-    const bf16_t* Dc = Ds + buf * QT;
-    bf16_t* Sc = St + buf * STT;
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      const int q0 = qbase + 32 * qb;
-      if (CAUSAL && q0 + 31 + off < kw0) continue;  // block fully masked: never read by dQ
-      // row constants as the initial accumulators: S - L/c and dP - delta come out of the
-      // MFMA chains ready for p = exp2(c s) and dS = p dp (no zero fill, no subtraction)
-      f32x16 s, dp;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 L = *reinterpret_cast<const f32x4*>(lse_s + buf * BMQ + 32 * qb + 8 * g4 + 4 * h32);
-        const f32x4 Dl = *reinterpret_cast<const f32x4*>(del_s + buf * BMQ + 32 * qb + 8 * g4 + 4 * h32);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { s[4 * g4 + j] = L[j]; dp[4 * g4 + j] = Dl[j]; }
-      }
-#pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        const int oq = loff<D>(32 * qb + l32, ks * 16 + 8 * h32);
-        // K from registers only where they fit (D = 64, causal), else from the LDS image
-        const bf16x8 kfr = KREG ? kf[ks] : lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
-        s = mfma32(lds_b128(Qc, oq), kfr, s);
-        dp = mfma32(lds_b128(Dc, oq), vf[ks], dp);
-        // D = 128: cap how far the scheduler hoists fragment reads (register pressure)
-        if constexpr (D == 128) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
-      }
-      const bool need_mask = (CAUSAL && (q0 + off < kw0 + 31)) || (kw0 + 32 > p.Tk) ||
-                             (q0 + 32 > p.T);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float pv = __builtin_amdgcn_exp2f(s[r] * c);
-        if (need_mask) {
-          const int q = q0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          if (mykey >= p.Tk || q >= p.T || (CAUSAL && mykey > q + off)) pv = 0.f;
-        }
-        s[r] = pv;
-        dp[r] = pv * dp[r];  // dS / scale
-      }
-      bf16x8 pb[2], sb[2];
-      pb[0] = acc_to_frag(s, 0);
-      pb[1] = acc_to_frag(s, 1);
-      sb[0] = acc_to_frag(dp, 0);
-      sb[1] = acc_to_frag(dp, 1);
-#pragma unroll
-      for (int db = 0; db < NDB; ++db) {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          dva[db] = mfma32(tr_frag<D>(Dc, 32 * qb + 16 * s2 + 4 * h32, db * 32, lane, 8), pb[s2], dva[db]);
-          dka[db] = mfma32(tr_frag<D>(Qc, 32 * qb + 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
-        }
-        if constexpr (D == 128) __builtin_amdgcn_sched_barrier(0);
-      }
-      // dS^T rows of the wave's 32 keys: registers 4g4..4g4+3 are q = 8 g4 + 4 h32 + 0..3
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        bf16x4 v4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = sb[g4 >> 1][4 * (g4 & 1) + j];
-        *reinterpret_cast<bf16x4*>(Sc + st_off<BMQ>(wv * 32 + l32, 32 * qb + 8 * g4 + 4 * h32)) = v4;
-      }
-    }
-    if (it + 1 < total) swrite(buf ^ 1);
-    lds_barrier();
-    // dQ tiles (16 q x 16 d) = dS K over the 256 keys, 32 keys per 16x16x32 MFMA.  Key
-    // steps above every q of the wave's rows are skipped (their dS rows are unwritten).
-    {
-      const int qr0 = qbase + 16 * qgw * TPW;   // first q row of the wave's tiles
-      int nks = BNK / 32;
-      if (CAUSAL) {
-        // last key of the workgroup any of these rows can see; negative = none (C division
-        // truncates toward zero, so the sign must be tested before dividing: with Tk > T a
-        // slice can start below the workgroup's first visible key)
-        const int last = qr0 + 16 * TPW - 1 + off - kt0;
-        nks = last < 0 ? 0 : min(nks, last / 32 + 1);
-      }
-      f32x4 dq[TPW];
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int g = lane >> 4, i = lane & 15;
-      for (int ks = 0; ks < nks; ++ks) {
-        const int kr = 32 * ks + 8 * g + (i >> 2);
-        const int dcol = 16 * d16w + 4 * (i & 3);
-        const bf16x8 bk = cat8(lds_tr(Ks, loff<D>(kr, dcol)), lds_tr(Ks, loff<D>(kr + 4, dcol)));
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const int qcol = 16 * (qgw * TPW + t) + 4 * (i & 3);
-          const bf16x8 a = cat8(lds_tr(Sc, st_off<BMQ>(kr, qcol)), lds_tr(Sc, st_off<BMQ>(kr + 4, qcol)));
-          dq[t] = mfma16(a, bk, dq[t]);
-        }
-      }
-      if (!(p.flags & 1) && nks > 0) {
-        float* dqg = p.dq_acc + (((long)b * p.Hq + hq) * p.T) * D + 16 * d16w + i;
-#pragma unroll
-        for (int t = 0; t < TPW; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = qbase + 16 * (qgw * TPW + t) + 4 * g + r;
-            if (q < p.T) atomicAdd(dqg + (long)q * D, dq[t][r] * p.scale);
-          }
-      }
-    }
-  };
-  for (int it = 0; it < total; it += 2) {
-    slice(it, std::integral_constant<int, 0>{});
-    if (it + 1 < total) slice(it + 1, std::integral_constant<int, 1>{});
-  }
-
-  // dK / dV: lane = key, registers = d ((r&3)+8(r>>2)+4*h32)
-  if (mykey < p.Tk) {
-    bf16_t* dKb = p.dk + b * p.dk_sb + hk * p.dk_sh + (long)mykey * p.dk_st;
-    bf16_t* dVb = p.dv + b * p.dv_sb + hk * p.dv_sh + (long)mykey * p.dv_st;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        bf16x4 k4, v4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          k4[j] = f2bf(dka[db][4 * g4 + j] * p.scale);
-          v4[j] = f2bf(dva[db][4 * g4 + j]);
-        }
-        *reinterpret_cast<bf16x4*>(dKb + db * 32 + 8 * g4 + 4 * h32) = k4;
-        *reinterpret_cast<bf16x4*>(dVb + db * 32 + 8 * g4 + 4 * h32) = v4;
-      }
-  }
-}
-
-// dq (bf16, strided) = dq_acc (fp32 [B][Hq][T][D])
 template <int D>
 __global__ __launch_bounds__(256) void attn_dq_convert_kernel(const float* __restrict__ acc,
                                                               bf16_t* __restrict__ dq, long sb,
@@ -837,11 +548,6 @@ static size_t bwd_lds(int D) {
   return 32 * nw * D * 2 + 4 * 32 * D * 2 + nw * 32 * 32 * 2 + 128 * 4 + nw * D * (32 + 4) * 4;
 }
 
-static size_t bwd2_lds(int D) {
-  const size_t bmq = D == 64 ? bwd2_bmq<64>() : bwd2_bmq<128>();
-  return (size_t)512 * D + 8 * bmq * D + 1024 * bmq + 16 * bmq;
-}
-
 template <int D, bool CAUSAL>
 static void set_lds_attr() {
   static bool done = false;
@@ -850,21 +556,8 @@ static void set_lds_attr() {
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)fwd_lds(D));
     hipFuncSetAttribute((const void*)attn_bwd_kernel<D, CAUSAL>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds(D));
-    if constexpr (D == 64)
-      hipFuncSetAttribute((const void*)attn_bwd2_kernel<D, CAUSAL>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd2_lds(D));
     done = true;
   }
-}
-
-// ORION_ATTN_BWD=v1 selects the 128-key backward (A/B measurement); default: 256-key v2
-static bool bwd_v2() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ORION_ATTN_BWD");
-    v = (e && e[0] == 'v' && e[1] == '1') ? 0 : 1;
-  }
-  return v == 1;
 }
 
 int orion_attn_fwd3(const AttnParams& p, int D, bool causal, hipStream_t st);  // attn_fwd.hip
@@ -909,16 +602,6 @@ int orion_attn_bwd(const AttnParams& p, int D, bool causal, float* delta, hipStr
   else return -1;
   AttnParams q = p;
   q.delta = delta;
-  // D = 128 stays on v1: the 8-wave form needs ~370 registers per lane there (110 spilled
-  // at the 256-register cap of two waves per SIMD) and the 4-wave form more than 512
-  if (bwd_v2() && D == 64) {
-#define BWD2(DD, CC)                                                                \
-  set_lds_attr<DD, CC>();                                                           \
-  attn_bwd2_kernel<DD, CC><<<((p.Tk + 255) / 256) * p.B * p.Hkv, BWD2_NW * 64, bwd2_lds(DD), st>>>(q);
-    if (causal) { BWD2(64, true) } else { BWD2(64, false) }
-#undef BWD2
-    return (int)hipGetLastError();
-  }
 #define BWD(DD, CC)                                                                 \
   set_lds_attr<DD, CC>();                                                           \
   attn_bwd_kernel<DD, CC><<<((p.Tk + 32 * bwd_waves<DD>() - 1) / (32 * bwd_waves<DD>())) * \

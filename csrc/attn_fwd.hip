@@ -20,7 +20,8 @@
 //
 // One workgroup = 4 waves = 128 query rows (32 per wave), key tiles of 64 double-buffered
 // in LDS, two workgroups per CU.  bf16 in / out, fp32 accumulation, O written as (B, T, H,
-// D), lse in base 2.  ORION_ATTN_FWD=v2 selects the older kernel (A/B measurement).
+// D), lse in base 2.  attention.hip's older forward remains the 64-bit-addressed fallback
+// (offsets past 2 GB; ORION_ATTN_FWD=v2 forces it for its test).
 #include <cstdlib>
 #include <type_traits>
 
@@ -322,12 +323,11 @@ int orion_attn_fwd3(const AttnParams& p, int D, bool causal, hipStream_t st) {
   const long kbytes = ((long)(p.Tk - 1) * p.k_st + D) * 2, vbytes = ((long)(p.Tk - 1) * p.v_st + D) * 2;
   if (kbytes >= (1L << 31) || vbytes >= (1L << 31)) return -2;
   const size_t lds = (size_t)2 * 2 * 64 * D * 2;
-  // D = 64 default: two 32-row query blocks per wave (one K / V fragment read for both, the
-  // two softmax chains interleaved with each other's MFMAs; 255 VGPRs).  Equal in isolation
-  // (0.208-0.211 vs 0.209-0.217 ms) but faster in the whole GPT-2 step in 8 of 8 alternating
-  // pairs on two boxes (+0.2-0.6 %, profiles/ab/ab_fwd_qb*.log).  ORION_FWD_QB=1: one block
-  // per wave (BM = 128).
-  static const int qb64 = getenv("ORION_FWD_QB") && getenv("ORION_FWD_QB")[0] == '1' ? 1 : 2;
+  // D = 64: two 32-row query blocks per wave (one K / V fragment read for both, the two
+  // softmax chains interleaved with each other's MFMAs; 255 VGPRs) -- equal in isolation to one
+  // block per wave but faster in the whole GPT-2 step in 8 of 8 alternating pairs on two boxes
+  // (+0.2-0.6 %, profiles/ab/ab_fwd_qb*.log); D = 128: one block per wave.
+  constexpr int qb64 = 2;
 #define FWD3(DD, CC) fwd3_launch<DD, CC>(p, qb64, lds, st);
   if (D == 64) {
     if (causal) { FWD3(64, true) } else { FWD3(64, false) }

@@ -58,6 +58,7 @@ int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, vo
                const void*, void*, long, const void*, long, hipStream_t, void* db = nullptr,
                int db_f32 = 0, float* part = nullptr);
 int orion_gemm_colsum_scratch(int M, int N);
+int orion_gemm_set_diag(int flags);
 
 namespace {
 
@@ -473,6 +474,10 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& sca
 
 int64_t wgrad_splits(int64_t M, int64_t N1, int64_t N2) { return orion_wgrad_splits(M, N1, N2); }
 
+// csrc/gemm.hip's diagnostic flags (stamps, one workgroup per work item): set in-process by
+// the benchmark / timeline scripts; returns the previous value
+int64_t gemm_diag(int64_t flags) { return orion_gemm_set_diag((int)flags); }
+
 // ------------------------------------------------------------------ GEMM (csrc/gemm.hip)
 // out (..., N) = x (..., K) . op(w) with op(w) = w^T for w (N, K) [w_kmajor = false, the
 // nn.Linear forward] or w for w (K, N) [w_kmajor = true, the input gradient], and a fused
@@ -508,7 +513,7 @@ std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor,
   }
   if (epi == 2) out2 = at::empty(sizes, x.options());
   if (epi == 0 && pre.has_value() && pre->defined() && pre->nbytes() >= 8 * 8 * 1024)
-    pp = pre->data_ptr();  // diagnostic: the ORION_GEMM_DIAG=4 slot-stamp buffer (scripts/gemm_stamps.py)
+    pp = pre->data_ptr();  // diagnostic: the gemm_diag(4) slot-stamp buffer (scripts/gemm16_stamps.py)
   if (epi == 3) {
     TORCH_CHECK(pre.has_value() && pre->defined(), "gemm: GELU backward needs the pre-activation");
     check_bf16(*pre, "pre");
@@ -526,7 +531,7 @@ std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor,
 
 // da = (dy . w) * GELU'(pre + bias) (w (K, N) k-major: the MLP output projection's weight
 // (C, F) read as the input gradient's operand) and db = colsum(da), the fused backward of
-// gelu(pre + bias) -> linear: csrc/gemm_phased.hip's EPI_GELU_BWD epilogue with per-64-row
+// gelu(pre + bias) -> linear: csrc/gemm16.hip's EPI_GELU_BWD epilogue with per-64-row
 // column-sum partials.  db goes into db_out (an fp32/bf16 gradient-arena slice) when given.
 std::tuple<Tensor, Tensor> gemm_gelu_bwd(const Tensor& dy, const Tensor& w, const Tensor& pre,
                                          const c10::optional<Tensor>& bias,
@@ -864,6 +869,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("wgrad(Tensor dy, Tensor x, Tensor? scale=None, int splits=0) -> Tensor");
   m.def("wgrad_into(Tensor dy, Tensor x, Tensor? scale, Tensor(a!) out, bool accumulate, int splits=0) -> ()");
   m.def("wgrad_splits(int M, int N1, int N2) -> int", &wgrad_splits);  // host-only helper
+  m.def("gemm_diag(int flags) -> int", &gemm_diag);                   // host-only helper
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");

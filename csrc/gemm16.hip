@@ -1,16 +1,16 @@
 // Phase-interleaved linear-layer GEMM on v_mfma_f32_16x16x32_bf16 (gfx950): forward (NT),
 // input gradient (NN) and weight gradient (k-major x k-major, split-K), fused epilogues.
+// Persistent: one workgroup per CU walks a list of work items with ONE continuous LDS-DMA
+// stream across them.
 //
-// Same tile, wave roles and barrier schedule as csrc/gemm_phased.hip (SCHED 1), with the
-// 16x16x32 MFMA instead of 32x32x16.  On random operands the chip holds a higher clock on the
-// 16x16x32 shape at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7:
-// ~1.12-1.15x FLOP/s in LDS-fed loops), which is the gap between the 32x32 phased kernel
-// (~1.15 PF/s at 4096^3) and the 16x16 8-phase template of the CDNA guide (~1.32 PF/s).
+// On random operands the chip holds a higher clock on the 16x16x32 shape than on 32x32x16 at
+// equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7: ~1.12-1.15x FLOP/s in
+// LDS-fed loops).
 //
-// Tile 256 (n) x 256 (m) per 512-thread workgroup, one workgroup per work item, K in 64-deep
-// k-tiles.  Swapped orientation: the W tile is the A operand (rows n), the X tile the B
-// operand (columns m), the accumulators hold C^T.  8 waves = 2 groups (grp = n half of 128) x
-// 4 (wm = 64 m rows); a wave owns 128 n x 64 m = 8 x 4 accumulators of 16 x 16.
+// Tile 256 (n) x 256 (m) per 512-thread workgroup, K in 64-deep k-tiles.  Swapped
+// orientation: the W tile is the A operand (rows n), the X tile the B operand (columns m),
+// the accumulators hold C^T.  8 waves = 2 groups (grp = n half of 128) x 4 (wm = 64 m rows);
+// a wave owns 128 n x 64 m = 8 x 4 accumulators of 16 x 16.
 //
 // Schedule (per k-tile, two phases H = 0, 1; group 1 runs one barrier slot behind group 0, so
 // on every SIMD one wave issues MFMAs while the other reads LDS and feeds the DMA):
@@ -18,8 +18,19 @@
 //     W n-half 1, 8) + this phase's LDS-DMA pieces, then s_waitcnt vmcnt(<this phase's>);
 //   MMA slot: wait lgkmcnt(0), 32 MFMAs (4 n-tiles x 4 m-tiles x 2 k-steps: 512 cycles).
 // Pieces (16 KB each, 2 buffer_load_dwordx4 ... lds per wave): A = W n-half 0, D = W n-half 1,
-// B / C = the two halves of the X image; A(t+1), B(t+2) issued in phase (t, 0), D(t+1), C(t+2)
-// in phase (t, 1).  X images triple-buffered, W double-buffered: 160 KB of LDS.
+// B / C = the two halves of the X image; A(s+1), B(s+2) issued in phase (s, 0), D(s+1), C(s+2)
+// in phase (s, 1).  X images triple-buffered, W double-buffered: 160 KB of LDS.
+//
+// Work walk (round 4).  A per-CU timeline of the one-workgroup-per-item launch at K = 768
+// (scripts/gemm16_timeline.py, profiles/gemm16/timeline_r04.txt) put 10-13 % of every CU's
+// time in the prologue (the first pieces' HBM latency, nothing to overlap it with), 15-18 %
+// in the epilogue and 3 % in workgroup dispatch.  Here the grid is at most one workgroup per
+// CU and s counts k-tiles over the workgroup's whole item list: the pieces of the next item's
+// first k-tiles are issued during the current item's last ones (the W stream runs one k-tile
+// ahead of the MFMAs, the X stream two), so only the first item pays a prologue, and the
+// epilogue of item j overlaps the DMA of item j + 1.  Items of one XCD: the blocks dealt to
+// an XCD (b % 8) share a contiguous range of work ids and walk it with stride (blocks on
+// that XCD), so the ~32 items an XCD runs at once stay neighbours in the grouped order (L2).
 //
 // LDS images, all lane-linear LDS-DMA destinations with the swizzle on the SOURCE address:
 //   NT operand ([rows][64 k], 128-byte rows): 16-byte chunk c of row r at c ^ ((r >> 1) & 7);
@@ -43,302 +54,42 @@ namespace {
 constexpr int G_BK = 64, G_IMG = 256 * G_BK;                 // bf16 elements per image
 constexpr int G_X0 = 0, G_W0 = 3 * G_IMG, G_LDS = 5 * G_IMG * 2;  // 160 KB
 
-ORION_DEVICE int nt_swz(int r) { return (r >> 1) & 7; }
-ORION_DEVICE int km_swz(int k) { return ((k >> 1) & 1) | (((k >> 3) & 1) << 1); }
-
-template <int OFF>
-ORION_DEVICE bf16x8 rd_b128(unsigned a) {
-  bf16x8 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
-  return r;
-}
-
-template <int OFF>
-ORION_DEVICE bf16x4 rd_tr(unsigned a) {
-  bf16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
-  return r;
-}
-
-ORION_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a),
-                                                 __builtin_bit_cast(bf16x8_mfma, b), c, 0, 0, 0);
-}
-
-ORION_DEVICE void g_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_barrier" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// all fragment reads of the phase retired; the fragments become "+v" operands of the wait so
-// no MFMA that uses them is scheduled above it
-ORION_DEVICE void g_wait_lds(bf16x8 (&a)[4][2]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]),
-                 "+v"(a[2][1]), "+v"(a[3][0]), "+v"(a[3][1]));
-}
-
 ORION_DEVICE f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-}  // namespace
+// one work item: output tile (m0, n0) and k chunk kc (split-K weight gradients)
+struct G16Item {
+  int m0, n0, kc, k0, kr, nk, rows_m, rows_n;
+};
 
-// STAMPS (diagnostic instantiation: ORION_GEMM_DIAG=4 with a stamp buffer, EPI_STORE only):
-// every wave of every workgroup records s_memtime at 16 points -- kernel start, prologue
-// landed, the 6 slot boundaries of both phases of the middle k-tile (READ start, reads+DMA
-// issued, vmcnt retired, MMA slot entered, fragments landed, MFMAs issued), main loop done,
-// epilogue issued -- into g.slabs as u64 [workgroup][wave][16] (scripts/gemm_stamps.py).
-template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
-__global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wv >> 2, wm = wv & 3;
-  const int q = lane >> 4, i16 = lane & 15;
-  [[maybe_unused]] unsigned long stp[16];
-  if constexpr (STAMPS) stp[0] = __builtin_amdgcn_s_memtime();
-
-  // work id: bijective XCD remap (blocks of one XCD get a contiguous range of work ids), then
+ORION_DEVICE G16Item g16_decode(const GemmArgs& g, int w) {
   // k chunk, then groups of GM m-tiles with the m-tile fastest (the ~32 tiles an XCD runs at
   // once share GM X panels and ~32 / GM W panels in its L2)
   constexpr int GM = 4;
-  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
-  const int qq = nwg >> 3, rr = nwg & 7;
-  int w = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int tiles_m = (g.M + 255) >> 8, tiles = tiles_m * g.tiles_n;
-  const int kc = w / tiles;
-  w -= kc * tiles;
+  G16Item it;
+  it.kc = w / tiles;
+  w -= it.kc * tiles;
   const int grp_sz = GM * g.tiles_n, gidx = w / grp_sz, first_m = gidx * GM;
   const int gm = min(tiles_m - first_m, GM), in = w - gidx * grp_sz;
-  const int m0 = (first_m + in % gm) * 256, n0 = (in / gm) * 256;
+  it.m0 = (first_m + in % gm) * 256;
+  it.n0 = (in / gm) * 256;
+  it.k0 = it.kc * g.kchunk;
+  it.kr = min(g.kchunk, g.K - it.k0);
+  it.nk = it.kr / G_BK;
+  it.rows_m = min(g.M - it.m0, 256);
+  it.rows_n = min(g.N - it.n0, 256);
+  return it;
+}
 
-  const int k0 = kc * g.kchunk, kr = min(g.kchunk, g.K - k0);
-  const int nk = kr / G_BK;
-  // buffer resources based at this work item's tile (rows m0 / n0) and k chunk, so only the
-  // tile's own extent has to fit the 32-bit offsets (a 6.6 GB logits operand is fine)
-  const int rows_m = min(g.M - m0, 256), rows_n = min(g.N - n0, 256);
-  __amdgpu_buffer_rsrc_t rx, rw;
-  if constexpr (XKM)
-    rx = make_rsrc(g.X + (long)k0 * g.ldx + m0, (unsigned)(((long)(kr - 1) * g.ldx + rows_m) * 2));
-  else
-    rx = make_rsrc(g.X + (long)m0 * g.ldx + k0, (unsigned)(((long)(rows_m - 1) * g.ldx + kr) * 2));
-  if constexpr (WKM)
-    rw = make_rsrc(g.W + (long)k0 * g.ldw + n0, (unsigned)(((long)(kr - 1) * g.ldw + rows_n) * 2));
-  else
-    rw = make_rsrc(g.W + (long)n0 * g.ldw + k0, (unsigned)(((long)(rows_n - 1) * g.ldw + kr) * 2));
-  const unsigned xstep = XKM ? (unsigned)(G_BK * g.ldx * 2) : G_BK * 2;
-  const unsigned wstep = WKM ? (unsigned)(G_BK * g.ldw * 2) : G_BK * 2;
+}  // namespace
 
-  // LDS-DMA of piece p (0 A, 1 B, 2 C, 3 D): this wave's blocks e = 0, 1 (one block = 8 image
-  // rows x 128 bytes = one wave instruction: lane -> row lane / 8, 16-byte slot lane % 8)
-  unsigned vo[4][2];
-  int ld[4][2];
-  {
-    const int lr = lane >> 3, slot = lane & 7;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int b = 2 * wm + e;  // 0..7
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {  // X pieces B (jj 0), C (jj 1)
-        if constexpr (XKM) {  // [64 k][64 m] image of wave row block wmp
-          const int wmp = 2 * jj + grp, k = 8 * b + lr;
-          const int m = m0 + wmp * 64 + 8 * (slot ^ (km_swz(k) << 1));
-          vo[1 + jj][e] = (unsigned)(((long)k * g.ldx + min(m, g.M - 8) - m0) * 2);
-          ld[1 + jj][e] = wmp * 4096 + 8 * b * 64;
-        } else {  // [256 m][64 k]: rows wm' 64 + 32 jj + [0, 32)
-          const int row0 = (2 * grp + (b >> 2)) * 64 + jj * 32 + (b & 3) * 8, row = row0 + lr;
-          const int ch = slot ^ nt_swz(row);
-          vo[1 + jj][e] = (unsigned)(((long)(min(m0 + row, g.M - 1) - m0) * g.ldx + 8 * ch) * 2);
-          ld[1 + jj][e] = row0 * 64;
-        }
-      }
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {  // W pieces A (n-half 0), D (n-half 1) of this group
-        const int p = hh ? 3 : 0;
-        if constexpr (WKM) {  // [64 k][64 n] image (grp, hh)
-          const int k = 8 * b + lr;
-          const int col = n0 + grp * 128 + hh * 64 + 8 * (slot ^ (km_swz(k) << 1));
-          vo[p][e] = (unsigned)(((long)k * g.ldw + min(col, g.N - 8) - n0) * 2);
-          ld[p][e] = (2 * grp + hh) * 4096 + 8 * b * 64;
-        } else {  // [256 n][64 k]: rows grp 128 + hh 64 + [0, 64)
-          const int row0 = grp * 128 + hh * 64 + b * 8, row = row0 + lr;
-          const int ch = slot ^ nt_swz(row);
-          vo[p][e] = (unsigned)(((long)(min(n0 + row, g.N - 1) - n0) * g.ldw + 8 * ch) * 2);
-          ld[p][e] = row0 * 64;
-        }
-      }
-    }
-  }
-  auto ximg = [&](int t) -> bf16_t* { return smem + G_X0 + (t % 3) * G_IMG; };
-  auto wimg = [&](int t) -> bf16_t* { return smem + G_W0 + (t & 1) * G_IMG; };
-  auto issue = [&](int p, int t) {
-    const bool isx = p == 1 || p == 2;
-    bf16_t* base = isx ? ximg(t) : wimg(t);
-    const unsigned so = (unsigned)t * (isx ? xstep : wstep);
-    ORION_DASSERT(t < nk);
-#pragma unroll
-    for (int e = 0; e < 2; ++e) blds16(isx ? rx : rw, vo[p][e], so, base + ld[p][e]);
-  };
-
-  // per-lane fragment offsets (bytes).  NT: row i16 of a 16-row tile, k chunk 4 s + q.
-  // k-major: rows 8 q + (i16 >> 2) (+ 4 for the second read, + 32 for k-step 1), columns
-  // 16 tile + 4 (i16 & 3) with the 32-byte segment (= tile) XOR the row swizzle.
-  int nto[2], kmo[4];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) nto[s] = i16 * 128 + (((4 * s + q) ^ nt_swz(i16)) << 4);
-  {
-    const int row0 = 8 * q + (i16 >> 2), h = km_swz(row0);
-#pragma unroll
-    for (int b = 0; b < 4; ++b) kmo[b] = row0 * 128 + ((b ^ h) << 5) + 8 * (i16 & 3);
-  }
-  const unsigned lds0 = lds_addr(smem, 0);
-
-  f32x4 acc[8][4];
-  // fragments: W [tile][k-step] (n-half 0 / 1), X [m-tile] of k-step 0 and of k-step 1
-  bf16x8 W0[4][2], W1[4][2], X0[4], X1[4];
-
-  // the wave's 4 m-tile fragments of k-step s of k-tile t
-  auto read_x = [&](bf16x8 (&Xd)[4], int t, auto Sc) {
-    constexpr int S = decltype(Sc)::value;
-    const unsigned base = lds0 + (unsigned)(ximg(t) - smem) * 2 + wm * 8192;
-    if constexpr (XKM) {
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const unsigned a = base + kmo[b];
-        Xd[b] = cat8(rd_tr<4096 * S>(a), rd_tr<4096 * S + 512>(a));
-      }
-    } else {
-      const unsigned a = base + nto[S];
-      Xd[0] = rd_b128<0>(a);
-      Xd[1] = rd_b128<2048>(a);
-      Xd[2] = rd_b128<4096>(a);
-      Xd[3] = rd_b128<6144>(a);
-    }
-  };
-  // W fragments of n-half H of k-tile t: 4 n-tiles x 2 k-steps
-  auto read_w = [&](bf16x8 (&Wf)[4][2], int t, auto Hc) {
-    constexpr int H = decltype(Hc)::value;
-    if constexpr (WKM) {
-      const unsigned base = lds0 + (unsigned)(wimg(t) - smem) * 2 + (2 * grp + H) * 8192;
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const unsigned ad = base + kmo[a];
-        Wf[a][0] = cat8(rd_tr<0>(ad), rd_tr<512>(ad));
-        Wf[a][1] = cat8(rd_tr<4096>(ad), rd_tr<4608>(ad));
-      }
-    } else {
-      const unsigned base = lds0 + (unsigned)(wimg(t) - smem) * 2 + grp * 16384 + H * 8192;
-      const unsigned a0 = base + nto[0], a1 = base + nto[1];
-      Wf[0][0] = rd_b128<0>(a0);
-      Wf[0][1] = rd_b128<0>(a1);
-      Wf[1][0] = rd_b128<2048>(a0);
-      Wf[1][1] = rd_b128<2048>(a1);
-      Wf[2][0] = rd_b128<4096>(a0);
-      Wf[2][1] = rd_b128<4096>(a1);
-      Wf[3][0] = rd_b128<6144>(a0);
-      Wf[3][1] = rd_b128<6144>(a1);
-    }
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I4 = std::integral_constant<int, 4>;
-  using Y = std::true_type;
-  using N = std::false_type;
-
-  [[maybe_unused]] const int tsel = nk / 2;
-  auto stamp = [&](int t, int k) {
-    if constexpr (STAMPS) {
-      if (t == tsel) stp[k] = __builtin_amdgcn_s_memtime();
-    }
-  };
-  // one phase: READ slot (fragments + pieces, then vmcnt(VMN) = this phase's own loads, so
-  // every older piece has landed before the next phase), MMA slot (32 MFMAs)
-  auto phase = [&](auto Hc, auto ISWc, auto ISXc, auto VMNc, int t) {
-    constexpr int H = decltype(Hc)::value, VMN = decltype(VMNc)::value;
-    constexpr bool ISW = decltype(ISWc)::value, ISX = decltype(ISXc)::value;
-    stamp(t, 2 + 6 * H);
-    if constexpr (H == 0) {
-      read_w(W0, t, Hc);
-      read_x(X0, t, I0());
-      read_x(X1, t, I1());
-      if constexpr (ISW) issue(0, t + 1);
-      if constexpr (ISX) issue(1, t + 2);
-    } else {
-      read_w(W1, t, Hc);
-      if constexpr (ISW) issue(3, t + 1);
-      if constexpr (ISX) issue(2, t + 2);
-    }
-    stamp(t, 3 + 6 * H);
-    wait_vm_exact<VMN>();
-    stamp(t, 4 + 6 * H);
-    g_barrier();
-    stamp(t, 5 + 6 * H);
-    // every fragment an MFMA of this slot reads is retired (and pinned behind the wait)
-    if constexpr (H == 0) {
-      g_wait_lds(W0);
-      asm volatile("" : "+v"(X0[0]), "+v"(X0[1]), "+v"(X0[2]), "+v"(X0[3]), "+v"(X1[0]),
-                   "+v"(X1[1]), "+v"(X1[2]), "+v"(X1[3]));
-    } else {
-      g_wait_lds(W1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    stamp(t, 6 + 6 * H);
-    bf16x8 (&Wf)[4][2] = H == 0 ? W0 : W1;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][0], X0[b], acc[4 * H + a][b]);
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][1], X1[b], acc[4 * H + a][b]);
-    __builtin_amdgcn_s_setprio(0);
-    stamp(t, 7 + 6 * H);
-    g_barrier();
-  };
-
-  // prologue: B0 C0 A0 D0 (B1 C1); phase (0, 0) needs the first three
-  issue(1, 0);
-  issue(2, 0);
-  issue(0, 0);
-  issue(3, 0);
-  if (nk > 1) {
-    issue(1, 1);
-    issue(2, 1);
-    wait_vm_exact<6>();
-  } else {
-    wait_vm_exact<2>();
-  }
-  if constexpr (STAMPS) stp[1] = __builtin_amdgcn_s_memtime();
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = zero4();
-  g_barrier();
-  if (grp == 1) g_barrier();  // the stagger: group 1 runs one slot behind
-
-  // steady state: k-tiles 0 .. nk - 3 issue pieces of t + 1 and t + 2; k-tile nk - 2 issues
-  // the W pieces of nk - 1; k-tile nk - 1 issues nothing
-  int t = 0;
-  for (; t < nk - 2; ++t) {
-    phase(I0(), Y(), Y(), I4(), t);
-    phase(I1(), Y(), Y(), I4(), t);
-  }
-  if (nk >= 2) {
-    phase(I0(), Y(), N(), I2(), t);
-    phase(I1(), Y(), N(), I2(), t);
-    ++t;
-  }
-  phase(I0(), N(), N(), I0(), t);
-  phase(I1(), N(), N(), I0(), t);
-  if (grp == 0) g_barrier();  // match group 1's barrier count
-  if constexpr (STAMPS) stp[14] = __builtin_amdgcn_s_memtime();
-
-  // ------------------------------------------------------------------ epilogue
+// The epilogue of one work item (registers only, no LDS).
+template <int EPI>
+ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16Item& it, int wm, int grp,
+                               int q, int i16) {
+  const int m0 = it.m0, kc = it.kc, rows_m = it.rows_m;
   const int mw = m0 + wm * 64;           // this wave's 64-row block
-  const int nw = n0 + grp * 128;         // this wave's 128 columns
+  const int nw = it.n0 + grp * 128;      // this wave's 128 columns
   if constexpr (EPI == EPI_WGRAD) {
     // fp32 partial tile into slab kc, or the final gradient (fp32 arena or bf16, scaled,
     // optionally accumulated): register quadruple = 4 consecutive n of row m
@@ -493,12 +244,328 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
       }
     }
   }
-  if constexpr (STAMPS) {
-    stp[15] = __builtin_amdgcn_s_memtime();
-    if (lane == 0) {
-      unsigned long* dst = reinterpret_cast<unsigned long*>(g.slabs) + ((long)blockIdx.x * 8 + wv) * 16;
+}
+
+// STAMPS (diagnostic instantiation: ORION_GEMM_DIAG=4 with a stamp buffer, EPI_STORE only,
+// one item per workgroup): every wave of every workgroup records s_memtime at 16 points --
+// kernel start, prologue landed, the 6 slot boundaries of both phases of the middle k-tile
+// (READ start, reads+DMA issued, vmcnt retired, MMA slot entered, fragments landed, MFMAs
+// issued), main loop done, epilogue issued -- plus where it ran (HW_ID / XCC_ID) into g.slabs
+// as u64 [workgroup][wave][20] (scripts/gemm16_stamps.py, scripts/gemm16_timeline.py).
+template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
+__global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wv >> 2, wm = wv & 3;
+  const int q = lane >> 4, i16 = lane & 15;
+  [[maybe_unused]] unsigned long stp[20];
+  if constexpr (STAMPS) stp[0] = __builtin_amdgcn_s_memtime();
+
+  // this workgroup's items: the work ids of XCD group b % 8 are one contiguous range of the
+  // grouped order (bijective split of `work` over 8), walked with stride = the number of
+  // blocks of that group; with one block per item (grid = work) each block gets one item
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, lcl = bid >> 3;
+  const int tiles_m = (g.M + 255) >> 8, work = tiles_m * g.tiles_n * g.ksplit;
+  const int wq = work >> 3, wr = work & 7;
+  const int r0 = xcd < wr ? xcd * (wq + 1) : wr * (wq + 1) + (xcd - wr) * wq;
+  const int rlen = wq + (xcd < wr ? 1 : 0);
+  const int stride = (nwg >> 3) + (xcd < (nwg & 7) ? 1 : 0);
+  const int nitems = lcl < rlen ? (rlen - lcl + stride - 1) / stride : 0;
+  if (nitems == 0) return;
+  auto item_id = [&](int j) { return r0 + lcl + j * stride; };
+
+  const unsigned xstep = XKM ? (unsigned)(G_BK * g.ldx * 2) : G_BK * 2;
+  const unsigned wstep = WKM ? (unsigned)(G_BK * g.ldw * 2) : G_BK * 2;
+
+  // LDS-DMA of piece p (0 A, 1 B, 2 C, 3 D): this wave's blocks e = 0, 1 (one block = 8 image
+  // rows x 128 bytes = one wave instruction: lane -> row lane / 8, 16-byte slot lane % 8).
+  // LDS destinations (ld) are item-independent; the source offsets (vo) and the buffer
+  // resources (based at the item's tile rows and k chunk, so only the tile's own extent has
+  // to fit the 32-bit offsets: a 6.6 GB logits operand is fine) are set per item, separately
+  // for the X stream and the W stream, which run ahead of the MFMAs by different amounts.
+  unsigned vo[4][2];
+  int ld[4][2];
+  __amdgpu_buffer_rsrc_t rx, rw;
+  const int lr = lane >> 3, slot = lane & 7;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) dst[k] = stp[k];
+  for (int e = 0; e < 2; ++e) {
+    const int b = 2 * wm + e;  // 0..7
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      if constexpr (XKM) ld[1 + jj][e] = (2 * jj + grp) * 4096 + 8 * b * 64;
+      else ld[1 + jj][e] = ((2 * grp + (b >> 2)) * 64 + jj * 32 + (b & 3) * 8) * 64;
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int p = hh ? 3 : 0;
+      if constexpr (WKM) ld[p][e] = (2 * grp + hh) * 4096 + 8 * b * 64;
+      else ld[p][e] = (grp * 128 + hh * 64 + b * 8) * 64;
+    }
+  }
+  auto setup_x = [&](const G16Item& it) {
+    if constexpr (XKM)
+      rx = make_rsrc(g.X + (long)it.k0 * g.ldx + it.m0, (unsigned)(((long)(it.kr - 1) * g.ldx + it.rows_m) * 2));
+    else
+      rx = make_rsrc(g.X + (long)it.m0 * g.ldx + it.k0, (unsigned)(((long)(it.rows_m - 1) * g.ldx + it.kr) * 2));
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int b = 2 * wm + e;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {  // X pieces B (jj 0), C (jj 1)
+        if constexpr (XKM) {  // [64 k][64 m] image of wave row block wmp
+          const int wmp = 2 * jj + grp, k = 8 * b + lr;
+          const int m = it.m0 + wmp * 64 + 8 * (slot ^ (km_swz(k) << 1));
+          vo[1 + jj][e] = (unsigned)(((long)k * g.ldx + min(m, g.M - 8) - it.m0) * 2);
+        } else {  // [256 m][64 k]: rows wm' 64 + 32 jj + [0, 32)
+          const int row0 = (2 * grp + (b >> 2)) * 64 + jj * 32 + (b & 3) * 8, row = row0 + lr;
+          const int ch = slot ^ nt_swz(row);
+          vo[1 + jj][e] = (unsigned)(((long)(min(it.m0 + row, g.M - 1) - it.m0) * g.ldx + 8 * ch) * 2);
+        }
+      }
+    }
+  };
+  auto setup_w = [&](const G16Item& it) {
+    if constexpr (WKM)
+      rw = make_rsrc(g.W + (long)it.k0 * g.ldw + it.n0, (unsigned)(((long)(it.kr - 1) * g.ldw + it.rows_n) * 2));
+    else
+      rw = make_rsrc(g.W + (long)it.n0 * g.ldw + it.k0, (unsigned)(((long)(it.rows_n - 1) * g.ldw + it.kr) * 2));
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int b = 2 * wm + e;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {  // W pieces A (n-half 0), D (n-half 1) of this group
+        const int p = hh ? 3 : 0;
+        if constexpr (WKM) {  // [64 k][64 n] image (grp, hh)
+          const int k = 8 * b + lr;
+          const int col = it.n0 + grp * 128 + hh * 64 + 8 * (slot ^ (km_swz(k) << 1));
+          vo[p][e] = (unsigned)(((long)k * g.ldw + min(col, g.N - 8) - it.n0) * 2);
+        } else {  // [256 n][64 k]: rows grp 128 + hh 64 + [0, 64)
+          const int row0 = grp * 128 + hh * 64 + b * 8, row = row0 + lr;
+          const int ch = slot ^ nt_swz(row);
+          vo[p][e] = (unsigned)(((long)(min(it.n0 + row, g.N - 1) - it.n0) * g.ldw + 8 * ch) * 2);
+        }
+      }
+    }
+  };
+  auto ximg = [&](int s) -> bf16_t* { return smem + G_X0 + (s % 3) * G_IMG; };
+  auto wimg = [&](int s) -> bf16_t* { return smem + G_W0 + (s & 1) * G_IMG; };
+
+  // the two issue streams: item index, k-tile within it, global k-tile counter (LDS buffer)
+  int jx = 0, tx = 0, sx = 0, jw = 0, tw = 0, sw = 0;
+  int nkx, nkw;
+  {
+    const G16Item it = g16_decode(g, item_id(0));
+    setup_x(it);
+    setup_w(it);
+    nkx = nkw = it.nk;
+  }
+  auto issue_x = [&](int jj) {  // piece B (jj 0) / C (jj 1) of the X stream's k-tile
+    ORION_DASSERT(jx < nitems && tx < nkx);
+    bf16_t* base = ximg(sx);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) blds16(rx, vo[1 + jj][e], (unsigned)tx * xstep, base + ld[1 + jj][e]);
+  };
+  auto issue_w = [&](int hh) {  // piece A (hh 0) / D (hh 1) of the W stream's k-tile
+    ORION_DASSERT(jw < nitems && tw < nkw);
+    bf16_t* base = wimg(sw);
+    const int p = hh ? 3 : 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) blds16(rw, vo[p][e], (unsigned)tw * wstep, base + ld[p][e]);
+  };
+  auto advance_x = [&]() {
+    ++sx;
+    if (++tx == nkx) {
+      tx = 0;
+      if (++jx < nitems) {
+        const G16Item it = g16_decode(g, item_id(jx));
+        setup_x(it);
+        nkx = it.nk;
+      }
+    }
+  };
+  auto advance_w = [&]() {
+    ++sw;
+    if (++tw == nkw) {
+      tw = 0;
+      if (++jw < nitems) {
+        const G16Item it = g16_decode(g, item_id(jw));
+        setup_w(it);
+        nkw = it.nk;
+      }
+    }
+  };
+
+  // per-lane fragment offsets (bytes).  NT: row i16 of a 16-row tile, k chunk 4 s + q.
+  // k-major: rows 8 q + (i16 >> 2) (+ 4 for the second read, + 32 for k-step 1), columns
+  // 16 tile + 4 (i16 & 3) with the 32-byte segment (= tile) XOR the row swizzle.
+  int nto[2], kmo[4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) nto[s] = i16 * 128 + (((4 * s + q) ^ nt_swz(i16)) << 4);
+  {
+    const int row0 = 8 * q + (i16 >> 2), h = km_swz(row0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) kmo[b] = row0 * 128 + ((b ^ h) << 5) + 8 * (i16 & 3);
+  }
+  const unsigned lds0 = lds_addr(smem, 0);
+
+  f32x4 acc[8][4];
+  // fragments: W [tile][k-step] (n-half 0 / 1), X [m-tile] of k-step 0 and of k-step 1
+  bf16x8 W0[4][2], W1[4][2], X0[4], X1[4];
+
+  // the wave's 4 m-tile fragments of k-step S of the k-tile in LDS buffer s
+  auto read_x = [&](bf16x8 (&Xd)[4], int s, auto Sc) {
+    constexpr int S = decltype(Sc)::value;
+    const unsigned base = lds0 + (unsigned)(ximg(s) - smem) * 2 + wm * 8192;
+    if constexpr (XKM) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const unsigned a = base + kmo[b];
+        Xd[b] = cat8(rd_tr<4096 * S>(a), rd_tr<4096 * S + 512>(a));
+      }
+    } else {
+      const unsigned a = base + nto[S];
+      Xd[0] = rd_b128<0>(a);
+      Xd[1] = rd_b128<2048>(a);
+      Xd[2] = rd_b128<4096>(a);
+      Xd[3] = rd_b128<6144>(a);
+    }
+  };
+  // W fragments of n-half H of the k-tile in buffer s: 4 n-tiles x 2 k-steps
+  auto read_w = [&](bf16x8 (&Wf)[4][2], int s, auto Hc) {
+    constexpr int H = decltype(Hc)::value;
+    if constexpr (WKM) {
+      const unsigned base = lds0 + (unsigned)(wimg(s) - smem) * 2 + (2 * grp + H) * 8192;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const unsigned ad = base + kmo[a];
+        Wf[a][0] = cat8(rd_tr<0>(ad), rd_tr<512>(ad));
+        Wf[a][1] = cat8(rd_tr<4096>(ad), rd_tr<4608>(ad));
+      }
+    } else {
+      const unsigned base = lds0 + (unsigned)(wimg(s) - smem) * 2 + grp * 16384 + H * 8192;
+      const unsigned a0 = base + nto[0], a1 = base + nto[1];
+      Wf[0][0] = rd_b128<0>(a0);
+      Wf[0][1] = rd_b128<0>(a1);
+      Wf[1][0] = rd_b128<2048>(a0);
+      Wf[1][1] = rd_b128<2048>(a1);
+      Wf[2][0] = rd_b128<4096>(a0);
+      Wf[2][1] = rd_b128<4096>(a1);
+      Wf[3][0] = rd_b128<6144>(a0);
+      Wf[3][1] = rd_b128<6144>(a1);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  int tsel = -1;
+  auto stamp = [&](int t, int k) {
+    if constexpr (STAMPS) {
+      if (t == tsel) stp[k] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  // one phase of global k-tile s (k-tile t of the current item): READ slot (fragments + the
+  // streams' pieces, then vmcnt(<this phase's own loads>), so every older piece has landed
+  // before the next phase), MMA slot (32 MFMAs)
+  auto phase = [&](auto Hc, int s, int t) {
+    constexpr int H = decltype(Hc)::value;
+    const bool isw = jw < nitems, isx = jx < nitems;
+    stamp(t, 2 + 6 * H);
+    if constexpr (H == 0) {
+      read_w(W0, s, Hc);
+      read_x(X0, s, I0());
+      read_x(X1, s, I1());
+    } else {
+      read_w(W1, s, Hc);
+    }
+    if (isw) issue_w(H);
+    if (isx) issue_x(H);
+    stamp(t, 3 + 6 * H);
+    if (isw && isx) wait_vm_exact<4>();
+    else if (isw || isx) wait_vm_exact<2>();
+    else wait_vm_exact<0>();
+    stamp(t, 4 + 6 * H);
+    g_barrier();
+    stamp(t, 5 + 6 * H);
+    // every fragment an MFMA of this slot reads is retired (and pinned behind the wait)
+    if constexpr (H == 0) {
+      g_wait_lds(W0);
+      asm volatile("" : "+v"(X0[0]), "+v"(X0[1]), "+v"(X0[2]), "+v"(X0[3]), "+v"(X1[0]),
+                   "+v"(X1[1]), "+v"(X1[2]), "+v"(X1[3]));
+    } else {
+      g_wait_lds(W1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    stamp(t, 6 + 6 * H);
+    bf16x8 (&Wf)[4][2] = H == 0 ? W0 : W1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][0], X0[b], acc[4 * H + a][b]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][1], X1[b], acc[4 * H + a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    stamp(t, 7 + 6 * H);
+    g_barrier();
+  };
+
+  // prologue: X k-tile 0 (B, C), W k-tile 0 (A, D), X k-tile 1 (B, C); phase (0, 0) needs the
+  // first three pieces
+  issue_x(0);
+  issue_x(1);
+  advance_x();
+  issue_w(0);
+  issue_w(1);
+  advance_w();
+  if (jx < nitems) {
+    issue_x(0);
+    issue_x(1);
+    advance_x();
+    wait_vm_exact<6>();
+  } else {
+    wait_vm_exact<2>();
+  }
+  if constexpr (STAMPS) stp[1] = __builtin_amdgcn_s_memtime();
+  g_barrier();
+  if (grp == 1) g_barrier();  // the stagger: group 1 runs one slot behind (kept across items)
+
+  int s = 0;
+  for (int j = 0; j < nitems; ++j) {
+    const G16Item it = g16_decode(g, item_id(j));
+    if constexpr (STAMPS) tsel = it.nk / 2;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = zero4();
+    for (int t = 0; t < it.nk; ++t, ++s) {
+      phase(I0(), s, t);
+      phase(I1(), s, t);
+      if (jw < nitems) advance_w();
+      if (jx < nitems) advance_x();
+    }
+    if constexpr (STAMPS) stp[14] = __builtin_amdgcn_s_memtime();
+    g16_epilogue<EPI>(g, acc, it, wm, grp, q, i16);
+  }
+  if (grp == 0) g_barrier();  // match group 1's barrier count
+  if constexpr (STAMPS) {
+    // 15: epilogue issued; 16: where the wave ran (HW_ID: cu / sh / se; XCC_ID); 17: its
+    // stores acknowledged (only with flags & 32, which waits for them: the default leaves the
+    // wave to end right after issuing, as the real kernel does)
+    stp[15] = __builtin_amdgcn_s_memtime();
+    stp[16] = (unsigned long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+              ((unsigned long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+    stp[17] = 0;
+    if (g.flags & 32) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stp[17] = __builtin_amdgcn_s_memtime();
+    }
+    if (lane == 0) {
+      unsigned long* dst = reinterpret_cast<unsigned long*>(g.slabs) + ((long)blockIdx.x * 8 + wv) * 20;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) dst[k] = stp[k];
     }
   }
 }
@@ -517,7 +584,11 @@ static int gemm16_launch(const GemmArgs& a, hipStream_t st) {
   }
   const long work = (long)((a.M + 255) / 256) * a.tiles_n * a.ksplit;
   if (work <= 0 || work > 0x7FFFFFFFL) return -1;
-  gemm16_kernel<XKM, WKM, EPI, STAMPS><<<(unsigned)work, 512, G_LDS, st>>>(a);
+  // persistent walk (one workgroup per CU) unless a stamped diagnostic or flags & 64 asks for
+  // one workgroup per item
+  const bool one_per_item = STAMPS || (a.flags & 64) || work <= 256;
+  const unsigned grid = one_per_item ? (unsigned)work : 256u;
+  gemm16_kernel<XKM, WKM, EPI, STAMPS><<<grid, 512, G_LDS, st>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -172,37 +172,20 @@ __global__ __launch_bounds__(WM * 256) void wgrad_kernel(
     }
 }
 
-// kernel configurations: {KS, NS}; LDS = NS * KS * 32 KB <= 160 KB
-// (A cross-stage fragment-prefetch variant -- barrier for stage t+1 before the MFMAs of
-// stage t, second fragment register set -- measured 0.77-0.79 PF/s vs 0.95-0.99 for
-// config 0 on MI355X and was removed; docs/PERFORMANCE.md.)
-struct WgCfg { int ks, ns, wm; };
-constexpr WgCfg WG_CFGS[] = {{2, 4, 4}, {2, 4, 2}, {4, 2, 2}, {2, 2, 4}};
-constexpr int WG_NCFG = sizeof(WG_CFGS) / sizeof(WG_CFGS[0]);
-
-// ORION_WGRAD_CFG: 9 = the 16x16x32-MFMA phased kernel (csrc/gemm16.hip, default: GPT-2 weight
-// gradients 4.9 vs 5.6 ms, whole step +3.9 %), 7 = the 32x32x16 phased kernel
-// (csrc/gemm_phased.hip), 0-3 =
-// wgrad_kernel configurations of WG_CFGS (read per call: microbenchmarks switch in-process)
-constexpr int WG_PHASED = 7;
-// (the phased kernel stages 64-token k-tiles: token counts that are not a multiple of 64
-// take wgrad_kernel's default configuration, which stages 32)
-static int wg_cfg(int M) {
-  const char* e = getenv("ORION_WGRAD_CFG");
-  int c = e ? atoi(e) : WG_PHASED + 2;
-  if (!(c == WG_PHASED || c == WG_PHASED + 1 || c == WG_PHASED + 2 || (c >= 0 && c < WG_NCFG)))
-    c = WG_PHASED + 2;
-  return c >= WG_PHASED && M % 64 ? 0 : c;
-}
-
 }  // namespace orion
 
 using namespace orion;
 
-static int wg_bk(int M) {
-  const int c = wg_cfg(M);
-  return c >= WG_PHASED ? 64 : 16 * WG_CFGS[c].ks;
-}
+// Two kernels serve the weight gradients:
+//   * csrc/gemm16.hip (EPI_WGRAD work items: k chunk x tile, v_mfma_f32_16x16x32_bf16,
+//     persistent walk) for every token count that is a multiple of 64 -- GPT-2 weight
+//     gradients 4.9 vs 5.6 ms for the 32x32x16 kernels it replaced, whole step +3.9 %;
+//   * wgrad_kernel above (32-row stages, configuration KS 2 / NS 4 / 16 waves) for the rest.
+// Round 4 removed the other wgrad_kernel configurations and the 32x32x16 phased kernel (no
+// default path selected them) and the per-call ORION_WGRAD_CFG lookup.
+constexpr int WG_KS = 2, WG_NS = 4, WG_WM = 4;
+
+static int wg_bk(int M) { return M % 64 ? 16 * WG_KS : 64; }
 
 // Split count: minimise (rounds of one-workgroup-per-CU) x (rows per workgroup) plus
 // the fp32 slab round trip, in units of rows of work.
@@ -217,7 +200,7 @@ int orion_wgrad_splits(int M, int N1, int N2) {
     if (chunk < 8 * BK && S > 1) break;
     const int Se = (M + chunk - 1) / chunk;
     if (Se != S) continue;
-    const long rounds = (tiles * Se + 255) / 256;  // one workgroup per CU (128 KB LDS)
+    const long rounds = (tiles * Se + 255) / 256;  // one workgroup per CU
     double cost = (double)rounds * chunk;
     if (Se > 1) cost += (double)Se * N1 * N2 * 8.0 / 5e12 * 1e9 / ns_per_row;
     if (cost < best * 0.98) {
@@ -236,12 +219,6 @@ int orion_wgrad_effective_splits(int M, int S) {
   return chunk > 0 ? (M + chunk - 1) / chunk : 1;
 }
 
-static int wgrad_lds(int M) {
-  if (wg_cfg(M) >= WG_PHASED) return 160 * 1024;
-  const WgCfg c = WG_CFGS[wg_cfg(M)];
-  return c.ns * c.ks * 16 * 128 * 4 * (int)sizeof(bf16_t);
-}
-
 // A (M x N1, ld lda), B (M x N2, ld ldb) bf16 -> slabs (S, N1, N2) fp32 when S > 1
 // (caller folds them), else out (N1, N2; fp32 when out_f32, else bf16) scaled by *scale
 // (nullable), added to the values already in out when accumulate != 0.
@@ -257,9 +234,8 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   if (S > 1 && !slabs) return -4;
   const int t1 = (N1 + 255) / 256, t2 = (N2 + 255) / 256;
   const int ntiles = t1 * t2;
-  if (wg_cfg(M) >= WG_PHASED) {
+  if (BK == 64 && (long)chunk * (lda > ldb ? lda : ldb) * 2 < 0xFFFFFF00L) {
     GemmArgs a{};
-    a.flags = wg_cfg(M) == WG_PHASED + 1 ? 16 : 0;  // (9: csrc/gemm16.hip)  // ORION_WGRAD_CFG=8: the 4-quadrant schedule
     a.X = (const bf16_t*)A;  // [M tokens][N1]: the k-major "X" operand, rows of out = N1
     a.ldx = lda;
     a.W = (const bf16_t*)B;  // [M tokens][N2]
@@ -276,33 +252,18 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
     a.scale = scale;
     a.accumulate = accumulate;
     a.out_f32 = out_f32;
-    if ((long)chunk * (lda > ldb ? lda : ldb) * 2 >= 0xFFFFFF00L) return -1;
-    if (wg_cfg(M) == WG_PHASED + 2) return gemm16_wgrad(a, st);  // ORION_WGRAD_CFG=9
-    return gemm_phased_wgrad(a, st);
+    return gemm16_wgrad(a, st);
   }
-  const int lds = wgrad_lds(M);
-  auto Ab = (const bf16_t*)A;
-  auto Bb = (const bf16_t*)B;
-  float* sl = S > 1 ? slabs : nullptr;
-#define WG_LAUNCH(KERNEL, KS, NS, WM)                                                           \
-  {                                                                                             \
-    static bool attr = false;                                                                   \
-    if (!attr) {                                                                                \
-      if (hipFuncSetAttribute((const void*)KERNEL<KS, NS, WM>,                                  \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)   \
-        return -5;                                                                              \
-      attr = true;                                                                              \
-    }                                                                                           \
-    KERNEL<KS, NS, WM><<<ntiles * S, WM * 256, lds, st>>>(Ab, lda, Bb, ldb, M, N1, N2, t2,       \
-                                                          ntiles, chunk, sl, out, scale,        \
-                                                          accumulate, out_f32);                 \
+  constexpr int lds = WG_NS * WG_KS * 16 * 128 * 4 * (int)sizeof(bf16_t);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)wgrad_kernel<WG_KS, WG_NS, WG_WM>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+      return -5;
+    attr = true;
   }
-  switch (wg_cfg(M)) {
-    case 0: WG_LAUNCH(wgrad_kernel, 2, 4, 4) break;  // measured best on MI355X (16 waves, 122 VGPR)
-    case 1: WG_LAUNCH(wgrad_kernel, 2, 4, 2) break;
-    case 2: WG_LAUNCH(wgrad_kernel, 4, 2, 2) break;
-    default: WG_LAUNCH(wgrad_kernel, 2, 2, 4) break;
-  }
-#undef WG_LAUNCH
+  wgrad_kernel<WG_KS, WG_NS, WG_WM><<<ntiles * S, WG_WM * 256, lds, st>>>(
+      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, M, N1, N2, t2, ntiles, chunk, S > 1 ? slabs : nullptr,
+      out, scale, accumulate, out_f32);
   return (int)hipGetLastError();
 }

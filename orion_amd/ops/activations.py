@@ -69,10 +69,13 @@ _FUSED_MLP = os.environ.get("ORION_FUSED_MLP", "1") != "0"
 def fused_mlp_ok(a, weight) -> bool:
     """The fused tail needs bf16 operands the in-tree GEMM takes: a (..., F) contiguous,
     weight (C, F) contiguous with C % 64 == 0 (the reduction dim of the input gradient)."""
+    from .gemm import gemm16_addressable
     return (_FUSED_MLP and a.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and a.is_contiguous() and weight.is_contiguous() and weight.shape[0] % 64 == 0
             and weight.shape[1] % 8 == 0 and a.data_ptr() % 16 == 0
-            and weight.data_ptr() % 16 == 0)
+            and weight.data_ptr() % 16 == 0
+            and gemm16_addressable(weight.shape[0], weight.shape[0], weight.shape[1], True)
+            and gemm16_addressable(weight.shape[1], weight.shape[1], weight.shape[0], False))
 
 
 class _GeluLinear(torch.autograd.Function):

@@ -1,22 +1,19 @@
-"""Weight-gradient GEMM dW = dY^T X (reduction over the token dimension).
+"""Linear-layer GEMMs: forward x W^T (+ bias), input gradient dy W, weight gradient dy^T x.
 
-Default path: the hand-written MFMA kernel of ``csrc/wgrad.hip`` (k-major operands
-through transposed LDS reads, split-K into fp32 slabs, XCD-aware tiles).  The
-``ORION_WGRAD=bmm`` path below is the library alternative it replaced, kept for
-A/B measurement:
+The in-tree kernel is ``csrc/gemm16.hip`` (v_mfma_f32_16x16x32_bf16, 256 x 256 tiles, one
+persistent 512-thread workgroup per CU walking its work items with one continuous LDS-DMA
+stream, fused bias / GELU / GELU' / column-sum epilogues).  It serves:
 
-dW = dY^T X reduces over all B*T tokens (65,536 rows for the GPT-2 bench) into
-a small output (768 x 768 ... 3072 x 768).  A single GEMM of that shape has only
-9-36 output tiles of 256 x 256 for 256 CUs, and hipBLASLt's picks run at
-0.4-0.8 PF/s on MI355X (`scripts/bench_wgrad.py`, profiles/wgrad_r01.json), well
-below the 1.3-1.6 PF/s of the forward GEMMs of the same layers.
+* every input gradient (``linear_dgrad``) and the fused MLP GEMMs (ops/activations.py);
+* every weight gradient (``wgrad`` / ``wgrad_into``: k-major operands, split-K work items
+  into fp32 slabs folded by ``slab_sum``, or straight into the fp32 gradient arena);
+* the plain forwards under ``ORION_GEMM=hip``, inside a HIP-graph capture (``hip_gemms()``)
+  and in the deterministic mode -- otherwise the plain forwards run on hipBLASLt
+  (``ORION_GEMM=auto``, the default; profiles/gemm16/).
 
-Here the token dimension is cut into S chunks and the chunks become the batch of
-ONE batched GEMM with fp32 output (S x more workgroups, no bf16 rounding of the
-partial sums), and a HIP kernel (`slab_sum`, csrc/activations.hip) folds the S
-fp32 slabs into the bf16 gradient in a fixed order, optionally times a device
-scalar (the LM head's loss scale).  Measured on MI355X at M = 65,536:
-768x768 0.20 -> 0.11 ms, 2304x768 0.39 -> 0.27 ms, 768x3072 0.41 -> 0.34 ms.
+``csrc/wgrad.hip`` keeps one MFMA weight-gradient kernel for token counts that are not a
+multiple of 64 (gemm16 stages 64-token k-tiles).  ``ORION_WGRAD=bmm`` is the library
+alternative (batched hipBLASLt GEMM over token chunks + ``slab_sum``), kept for A/B runs.
 """
 from __future__ import annotations
 
@@ -30,16 +27,11 @@ from .determinism import deterministic
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
 # Linear-layer forward (x W^T [+ b]) and input gradient (dy W).  ORION_GEMM=auto (default):
-# every input gradient on the in-tree 16x16x32-MFMA kernel (csrc/gemm16.hip: the GPT-2 qkv /
-# attn-proj / fc / LM-head dgrads run 4-25 % faster than hipBLASLt in isolation,
-# profiles/gemm16/), plain forward GEMMs on hipBLASLt (the in-tree kernel loses 1-10 % there
-# and 45 % on the K = 768 LM head).  ORION_GEMM=blas: hipBLASLt for all; ORION_GEMM=hip: every
-# eligible GEMM in-tree.  Whole GPT-2 step, same box, 3 alternating runs
-# (profiles/ab/ab_gemm_auto_fusedmlp_r03e.log): blas 1,047.7-1,048.8k, auto 1,045.6-1,048.8k,
-# auto + fused MLP (ops/activations.py) 1,048.5-1,054.9k, hip + fused MLP 1,009.4-1,012.3k
-# tok/s.  Inside a HIP-graph capture (``hip_gemms()``) every eligible GEMM is in-tree (no
-# library-side host state between replays), and so in the deterministic mode
-# (ops/determinism.py): one workgroup per output tile, no split-K.
+# every input gradient on csrc/gemm16.hip, plain forward GEMMs on hipBLASLt.
+# ORION_GEMM=blas: hipBLASLt for all; ORION_GEMM=hip: every eligible GEMM in-tree.  Inside a
+# HIP-graph capture (``hip_gemms()``) every eligible GEMM is in-tree (no library-side host
+# state between replays), and so in the deterministic mode (ops/determinism.py): one work
+# item per output tile, no split-K.
 _GEMM_IMPL = os.environ.get("ORION_GEMM", "auto")  # "auto" | "blas" | "hip"
 _FORCE_HIP = 0
 
@@ -55,7 +47,8 @@ _FORCED_FALLBACKS: list = []
 
 @contextlib.contextmanager
 def hip_gemms():
-    """Route eligible linear-layer GEMMs to csrc/gemm.hip inside the block."""
+    """Route eligible linear-layer GEMMs to the in-tree kernel (csrc/gemm16.hip) inside the
+    block: a captured HIP graph then holds no library GEMM (no library-side host state)."""
     global _FORCE_HIP
     _FORCE_HIP += 1
     try:
@@ -77,13 +70,27 @@ def _note_fallback(kind: str, *tensors):
         _FORCED_FALLBACKS.append((kind, tuple(tuple(t.shape) for t in tensors)))
 
 
+_OFF_LIMIT = 0xFFFFFF00  # gemm16's buffer resources: 32-bit byte offsets per work item
+
+
+def gemm16_addressable(ldx: int, K: int, N: int, w_kmajor: bool) -> bool:
+    """csrc/gemm16.hip bases its buffer resources at the work item's tile: one 256-row band
+    of X / the outputs / the pre-activation, and the whole [K][N] weight when it is k-major,
+    must fit 32-bit offsets (gemm16_ok).  Outside that the caller takes hipBLASLt."""
+    bands = 256 * 2 * max(ldx, N, 1)
+    wb = K * N * 2 if w_kmajor else 256 * 2 * K
+    return bands < _OFF_LIMIT and wb < _OFF_LIMIT
+
+
 def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
     K = x.shape[-1]
     N = w.shape[1] if w_kmajor else w.shape[0]
+    ldx = x.stride(0) if x.dim() == 2 else K
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and K % 64 == 0 and N % 8 == 0 and w.is_contiguous() and x.stride(-1) == 1
             and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
-            and (x.dim() == 2 and x.stride(0) % 8 == 0 or x.is_contiguous()))
+            and (x.dim() == 2 and x.stride(0) % 8 == 0 or x.is_contiguous())
+            and gemm16_addressable(ldx, K, N, w_kmajor))
 
 
 def _hip_wins(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
@@ -102,7 +109,7 @@ def use_hip_gemm(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
 
 
 def linear_fwd(x, w, b=None):
-    """x W^T (+ b): csrc/gemm.hip when selected (see above), else hipBLASLt."""
+    """x W^T (+ b): csrc/gemm16.hip when selected (see above), else hipBLASLt."""
     if use_hip_gemm(x, w, False):
         return C().gemm(x, w, False, EPI_BIAS if b is not None else EPI_STORE, b, None)[0]
     _note_fallback("linear_fwd", x, w)
@@ -124,7 +131,7 @@ def linear_dgrad(dy, w):
 WGRAD_FIRST = os.environ.get("ORION_WGRAD_FIRST", "0") == "1"
 
 _FORCE = os.environ.get("ORION_WGRAD_SPLITS")
-_IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/gemm_phased.hip) | "blas" | "bmm"
+_IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/gemm16.hip) | "blas" | "bmm"
 
 
 def _hip_ok(dy, x):
@@ -149,11 +156,9 @@ def wgrad_splits(M: int, n1: int, n2: int) -> int:
 
 
 def _blas_wins(n1: int, n2: int) -> bool:
-    """hipBLASLt for the weight gradient only when asked (ORION_WGRAD=blas): the phased kernel
-    of csrc/gemm_phased.hip beats it on every measured shape -- GPT-2 (1.3-2x) and the
-    Llama-7B shapes at 16k tokens (12288/4096/22016/32000 x 4096 and 4096 x 11008: 9.8 vs
-    10.75 ms in total, profiles/gemm_study/bench_wgrad_llama_shapes.log), where csrc/wgrad.hip
-    used to lose by 5-12 %."""
+    """hipBLASLt for the weight gradient only when asked (ORION_WGRAD=blas): the in-tree
+    kernel beats it on every measured shape -- GPT-2 (1.3-2x) and the Llama-7B shapes at 16k
+    tokens (profiles/gemm16/bench_wgrad_gemm16_vs_gemm32*.log)."""
     return _IMPL == "blas" and not deterministic() and not _FORCE_HIP
 
 

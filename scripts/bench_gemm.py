@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """GEMM microbenchmark on the GPT-2-124M training shapes (M = 64 x 1024 tokens):
-csrc/gemm.hip (with its fused epilogues) vs hipBLASLt through PyTorch (committed TunableOp
+csrc/gemm16.hip (with its fused epilogues) vs hipBLASLt through PyTorch (committed TunableOp
 table loaded) plus the separate HIP epilogue kernels it needs.  Interleaved rounds in one
 process, median per variant; one JSON line per shape.
 
@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--M", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--check", action="store_true", help="compare outputs against torch")
-    ap.add_argument("--cfgs", default="7", help="comma list of ORION_GEMM_CFG variants to time (7 = phased)")
+    ap.add_argument("--cfgs", default="p", help="comma list of in-tree variants to time: p = gemm16's "
+                    "persistent walk (default), s = one workgroup per work item (gemm_diag(64))")
     ap.add_argument("--square", type=int, default=0, help="also time an NT GEMM of this cube size")
     ap.add_argument("--only", default="", help="comma list of shape names to run")
     ap.add_argument("--llama", action="store_true", help="Llama-2-7B shapes (M = 16,384 tokens) instead")
@@ -102,7 +103,7 @@ def main():
                 blas = lambda: x @ w
         def with_cfg(c, f):
             def run():
-                os.environ["ORION_GEMM_CFG"] = c
+                ops.gemm_diag(64 if c == "s" else 0)
                 return f()
             return run
         fns = {f"hip{c}": with_cfg(c, hip) for c in cfgs}
@@ -119,8 +120,7 @@ def main():
             ref = (x.float() @ (w.float().t() if kind == "fwd" else w.float()))
             if b is not None and epi != 5:
                 ref = ref + b.float()
-            os.environ["ORION_GEMM_CFG"] = cfgs[0]
-            got = hip()
+            got = with_cfg(cfgs[0], hip)()
             o = got[0].float()
             if epi in (3, 5):
                 from orion_amd.ops import reference as R

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Slot anatomy of csrc/gemm16.hip from its stamped diagnostic instantiation
-(ORION_GEMM_CFG=9, ORION_GEMM_DIAG=4): every wave of every workgroup stamps s_memtime at
+(gemm_diag(4)): every wave of every workgroup stamps s_memtime at
 kernel start, prologue landed, the six slot boundaries of both phases of the middle k-tile,
 main-loop end and epilogue end.  Prints medians (cycles) per group and phase over all
 workgroups: reads+DMA issue, vmcnt wait, barrier wait into the MMA slot, lgkmcnt wait, MFMA
@@ -17,21 +17,20 @@ from orion_amd.ops._ext import C, load_ext  # noqa: E402
 
 M, N, K, wkm = (int(v) for v in sys.argv[1:5])
 load_ext(required=True)
-os.environ["ORION_GEMM_CFG"] = "9"
 g = torch.Generator(device="cuda").manual_seed(0)
 x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
 w = (torch.randn(*((K, N) if wkm else (N, K)), device="cuda", generator=g) * 0.5).to(torch.bfloat16)
 nwg = ((M + 255) // 256) * ((N + 255) // 256)
-buf = torch.zeros(nwg * 8 * 16, device="cuda", dtype=torch.int64)
-os.environ["ORION_GEMM_DIAG"] = "0"
+buf = torch.zeros(nwg * 8 * 20, device="cuda", dtype=torch.int64)
+C().gemm_diag(0)
 for _ in range(10):
     C().gemm(x, w, bool(wkm), 0, None, None)
-os.environ["ORION_GEMM_DIAG"] = "4"
+C().gemm_diag(4)
 for _ in range(3):
     C().gemm(x, w, bool(wkm), 0, None, buf)
 torch.cuda.synchronize()
-os.environ["ORION_GEMM_DIAG"] = "0"
-st = buf.view(nwg, 8, 16).cpu()
+C().gemm_diag(0)
+st = buf.view(nwg, 8, 20)[:, :, :16].cpu()
 rec = {"shape": f"{M}x{N}x{K}x{wkm}", "workgroups": nwg}
 names = ["issue", "vmcnt", "bar_in", "lgkm", "mfma", "bar_out"]
 for grp in (0, 1):

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Run one csrc/gemm.hip shape a few times (for rocprofv3 --pmc passes).
+"""Run one csrc/gemm16.hip shape a few times (for rocprofv3 --pmc passes).
 usage: python scripts/gemm_one.py M N K wkm epi [reps] [blas]
 (blas = 1: the same product through torch / hipBLASLt with the committed TunableOp table)"""
 import os

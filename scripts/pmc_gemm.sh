@@ -1,6 +1,6 @@
 #!/bin/bash
-# PMC counter passes (kernel-trace only, each pass its own run) for one csrc/gemm.hip shape.
-# usage: scripts/pmc_gemm.sh TAG M N K wkm epi   (ORION_GEMM_CFG selects the kernel variant)
+# PMC counter passes (kernel-trace only, each pass its own run) for one csrc/gemm16.hip shape.
+# usage: scripts/pmc_gemm.sh TAG M N K wkm epi
 set -o pipefail
 cd "$(dirname "$0")/.."
 REPO=$(pwd)

@@ -1,20 +1,20 @@
-"""The linear-layer GEMMs (csrc/gemm_phased.hip by default, csrc/gemm.hip's 2-stage kernel
-under ORION_GEMM_CFG=0; forward NT / input-gradient NN with fused epilogues) against an fp32
-PyTorch reference, including ragged M and N (partial 256 x 256 tiles), more tiles than CUs
-(the persistent tile walk: 777 x 50304) and the epilogues (bias, bias + GELU with the
-pre-activation output, GELU backward)."""
+"""The linear-layer GEMMs of csrc/gemm16.hip (forward NT / input-gradient NN with fused
+epilogues, weight gradients with split-K) against an fp32 PyTorch reference, including ragged
+M and N (partial 256 x 256 tiles), more work items than CUs (the persistent walk: 777 x 50304
+has 4 x 197 items for 256 workgroups, i.e. items of different lengths meet inside one
+workgroup's continuous DMA stream) and the epilogues (bias, bias + GELU with the
+pre-activation output, GELU backward with column sums).  Every shape runs on the persistent
+walk (the default) and with one workgroup per work item (gemm_diag(64)).  Error budgets: the
+in-tree result may be at most 2x as far from fp32 as the same product in stock PyTorch bf16
+(tests/tolerance.py)."""
 import pytest
 import torch
 
 from orion_amd.ops import reference as ref
+from tolerance import rel_err, within_bf16_budget
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-
-
-def rel_err(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
 def _C():
@@ -32,15 +32,18 @@ def _gelu_grad(z):
 
 
 SHAPES = [(256, 256, 64), (300, 264, 128), (1000, 768, 768), (513, 1000, 192), (64, 8, 64),
-          (4096, 2304, 768), (2048, 3072, 768), (1024, 768, 3072), (777, 50304, 128)]
+          (4096, 2304, 768), (2048, 3072, 768), (1024, 768, 3072), (777, 50304, 128),
+          (65536, 768, 768)]
 
 
-@pytest.fixture(params=["7", "9"], ids=["mfma32", "mfma16"])
-def gemm_cfg(request, monkeypatch):
-    """The phased kernel on v_mfma_f32_32x32x16 (csrc/gemm_phased.hip, 7) and on
-    v_mfma_f32_16x16x32 (csrc/gemm16.hip, 9)."""
-    monkeypatch.setenv("ORION_GEMM_CFG", request.param)
-    return request.param
+@pytest.fixture(params=["persistent", "per_item"])
+def gemm_cfg(request):
+    """gemm16's persistent walk (one workgroup per CU, continuous DMA stream across items)
+    and the one-workgroup-per-item launch (diagnostic flag 64)."""
+    C = _C()
+    old = C.gemm_diag(64 if request.param == "per_item" else 0)
+    yield request.param
+    C.gemm_diag(old)
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
@@ -52,7 +55,7 @@ def test_gemm_store(M, N, K, wkm, gemm_cfg):
     out, _ = _C().gemm(x, w, wkm, 0, None, None)
     want = x.float() @ (w.float() if wkm else w.float().t())
     assert out.shape == (M, N)
-    assert rel_err(out, want) < 1e-2
+    within_bf16_budget("out", out, want, x @ (w if wkm else w.t()))
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES[:6])
@@ -60,11 +63,12 @@ def test_gemm_bias_and_bias_gelu(M, N, K, gemm_cfg):
     g = torch.Generator(device=DEV).manual_seed(7 + M)
     x, w, b = _rnd(g, M, K), _rnd(g, N, K), _rnd(g, N)
     a = x.float() @ w.float().t() + b.float()
+    ab = torch.nn.functional.linear(x, w, b)
     out, none = _C().gemm(x, w, False, 1, b, None)
-    assert rel_err(out, a) < 1e-2
+    within_bf16_budget("bias", out, a, ab)
     pre, h = _C().gemm(x, w, False, 2, b, None)
-    assert rel_err(pre, a) < 1e-2
-    assert rel_err(h, ref.gelu_tanh(a)) < 1e-2
+    within_bf16_budget("pre", pre, a, ab)
+    within_bf16_budget("gelu", h, ref.gelu_tanh(a), torch.nn.functional.gelu(ab, approximate="tanh"))
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES[:6])
@@ -73,35 +77,37 @@ def test_gemm_gelu_backward_epilogue(M, N, K, gemm_cfg):
     dy, w, pre = _rnd(g, M, K), _rnd(g, K, N), _rnd(g, M, N)
     out, _ = _C().gemm(dy, w, True, 3, None, pre)
     want = (dy.float() @ w.float()) * _gelu_grad(pre.float())
-    assert rel_err(out, want) < 1e-2
+    within_bf16_budget("da", out, want, (dy @ w) * _gelu_grad(pre.float()).bfloat16())
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 768), (4096, 3072, 768), (777, 264, 128)])
-@pytest.mark.parametrize("cfg", ["9", "7", "8", "0"])
 @pytest.mark.parametrize("arena", [None, torch.float32, torch.bfloat16])
-def test_gemm_gelu_bwd_with_bias_grad(M, N, K, cfg, arena, monkeypatch):
+def test_gemm_gelu_bwd_with_bias_grad(M, N, K, arena, gemm_cfg):
     """gemm_gelu_bwd: da = (dy w) * GELU'(pre + b) and db = colsum(da) (per-64-row partials
-    from the phased kernel's epilogue, cfg 7/8; a column-sum pass after csrc/gemm.hip's
-    kernel, cfg 0), db returned or written into a gradient-arena slice."""
-    monkeypatch.setenv("ORION_GEMM_CFG", cfg)
+    from gemm16's epilogue, folded by a second pass), db returned or written into a
+    gradient-arena slice."""
     g = torch.Generator(device=DEV).manual_seed(M + N + 5 * K)
     dy, w, pre, b = _rnd(g, M, K), _rnd(g, K, N), _rnd(g, M, N), _rnd(g, N)
-    want = (dy.float() @ w.float()) * _gelu_grad(pre.float() + b.float())
+    gp = _gelu_grad(pre.float() + b.float())
+    want = (dy.float() @ w.float()) * gp
+    base = (dy @ w) * gp.bfloat16()
     out = None if arena is None else torch.full((N,), 7.0, device=DEV, dtype=arena)
     da, db = _C().gemm_gelu_bwd(dy, w, pre, b, out)
-    assert rel_err(da, want) < 1e-2
+    within_bf16_budget("da", da, want, base)
     got = db if arena is None else out
     assert (db is None or db.numel() == 0) if arena is not None else db.shape == (N,)
-    assert rel_err(got, want.sum(0)) < 1e-2
+    within_bf16_budget("db", got, want.sum(0), base.float().sum(0).to(arena or torch.bfloat16))
 
 
 def test_gemm_gelu_bwd_without_bias():
     g = torch.Generator(device=DEV).manual_seed(21)
     dy, w, pre = _rnd(g, 640, 256), _rnd(g, 256, 512), _rnd(g, 640, 512)
     da, db = _C().gemm_gelu_bwd(dy, w, pre, None, None)
-    want = (dy.float() @ w.float()) * _gelu_grad(pre.float())
-    assert rel_err(da, want) < 1e-2
-    assert rel_err(db, want.sum(0)) < 1e-2
+    gp = _gelu_grad(pre.float())
+    want = (dy.float() @ w.float()) * gp
+    base = (dy @ w) * gp.bfloat16()
+    within_bf16_budget("da", da, want, base)
+    within_bf16_budget("db", db, want.sum(0), base.float().sum(0).bfloat16())
 
 
 @pytest.mark.parametrize("fuse_out_bias", [False, True])
@@ -146,13 +152,18 @@ def test_fused_mlp_matches_reference(proj_bias, fc_bias, monkeypatch):
     a = fs[0] @ fs[1].t() + (fs[2] if fc_bias else 0)
     yr = ref.gelu_tanh(a) @ fs[3].t() + (fs[4] if proj_bias else 0)
     yr.backward(dy.float())
-    assert rel_err(y, yr) < 1e-2
+    bs = [t.detach().clone().requires_grad_() for t in (x, wfc, bfc, wp, bp)]
+    F = torch.nn.functional
+    yb = F.linear(F.gelu(F.linear(bs[0], bs[1], bs[2] if fc_bias else None), approximate="tanh"),
+                  bs[3], bs[4] if proj_bias else None)
+    yb.backward(dy)
+    within_bf16_budget("y", y, yr, yb)
     names = ["dx", "dwfc", "dbfc", "dwproj", "dbproj"]
-    for i, (n, t, f) in enumerate(zip(names, ts, fs)):
+    for i, (n, t, f, bb) in enumerate(zip(names, ts, fs, bs)):
         if (i == 2 and not fc_bias) or (i == 4 and not proj_bias):
             assert t.grad is None
             continue
-        assert rel_err(t.grad, f.grad) < 2e-2, (n, rel_err(t.grad, f.grad))
+        within_bf16_budget(n, t.grad, f.grad, bb.grad)
 
 
 def test_gemm_batched_input_shape_and_strided_rows():
@@ -161,41 +172,28 @@ def test_gemm_batched_input_shape_and_strided_rows():
     w = _rnd(g, 512, 256)
     out, _ = _C().gemm(x, w, False, 0, None, None)
     assert out.shape == (4, 96, 512)
-    assert rel_err(out, x.float() @ w.float().t()) < 1e-2
+    within_bf16_budget("out", out, x.float() @ w.float().t(), x @ w.t())
     big = _rnd(g, 300, 2304)           # a column slice of a wider buffer (row stride 2304)
     xs = big[:, 768:1536]
-    out2, _ = _C().gemm(xs, w[:, :256].contiguous().repeat(1, 3), False, 0, None, None)
-    assert rel_err(out2, xs.float() @ w[:, :256].float().repeat(1, 3).t()) < 1e-2
+    w3 = w[:, :256].contiguous().repeat(1, 3)
+    out2, _ = _C().gemm(xs, w3, False, 0, None, None)
+    within_bf16_budget("strided", out2, xs.float() @ w3.float().t(), xs @ w3.t())
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 264, 128), (1000, 768, 768), (777, 50304, 128)])
-@pytest.mark.parametrize("wkm", [False, True])
-@pytest.mark.parametrize("cfg", ["0", "8", "7", "9"])
-def test_gemm_other_schedules(M, N, K, wkm, cfg, monkeypatch):
-    """csrc/gemm.hip's 2-stage kernel (ORION_GEMM_CFG=0) and the phased kernel's 4-quadrant
-    schedule (8); the variable is read per call."""
-    monkeypatch.setenv("ORION_GEMM_CFG", cfg)
-    g = torch.Generator(device=DEV).manual_seed(M + 3 * N + K)
-    x = _rnd(g, M, K)
-    w = _rnd(g, K, N) if wkm else _rnd(g, N, K)
-    out, _ = _C().gemm(x, w, wkm, 0, None, None)
-    assert rel_err(out, x.float() @ (w.float() if wkm else w.float().t())) < 1e-2
-
-
-@pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768), (8224, 200, 264)])
-@pytest.mark.parametrize("cfg", ["9", "7", "8", "0"])
+@pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768), (8224, 200, 264),
+                                     (16384, 50304, 768)])
 @pytest.mark.parametrize("acc", [False, True])
-def test_wgrad_phased_and_two_stage_into_fp32(M, N1, N2, cfg, acc, monkeypatch):
-    """Weight gradients on the phased kernel (split-K work items, fp32 slabs) and on
-    csrc/wgrad.hip (ORION_WGRAD_CFG=0) into an fp32 arena slice, overwrite and accumulate
-    (8224 tokens: not a multiple of 64, so the phased default hands over to csrc/wgrad.hip)."""
-    monkeypatch.setenv("ORION_WGRAD_CFG", cfg)
+def test_wgrad_into_fp32(M, N1, N2, acc, gemm_cfg):
+    """Weight gradients on gemm16 (split-K work items into fp32 slabs, or straight into the
+    arena) into an fp32 arena slice, overwrite and accumulate; 8224 tokens (not a multiple of
+    64) take csrc/wgrad.hip's 32-row kernel; 50,304 x 768 is the LM head."""
     g = torch.Generator(device=DEV).manual_seed(M + N1)
     dy, x = _rnd(g, M, N1), _rnd(g, M, N2)
     out = torch.randn(N1, N2, device=DEV, generator=g)
     base = out.clone()
     _C().wgrad_into(dy, x, None, out, acc, 0)
     want = dy.float().t() @ x.float() + (base if acc else 0)
+    # fp32 output, fp32 accumulation: far below any bf16 budget
     assert rel_err(out, want) < 1e-4
 
 
@@ -205,16 +203,15 @@ def test_gemm16_operands_past_4gb(wkm, monkeypatch):
     operand (the LM head's logits: 65,536 x 50,304 bf16 = 6.6 GB) stays on the kernel: the
     forward writes a 4.4 GB output, the input gradient reads a 4.4 GB operand.  Rows at both
     ends checked against fp32."""
-    monkeypatch.setenv("ORION_GEMM_CFG", "9")
     g = torch.Generator(device=DEV).manual_seed(7)
     M, V = 43776, 50304
     if not wkm:  # out (M, V) = x (M, 64) W (V, 64)^T
         x, w = _rnd(g, M, 64), _rnd(g, V, 64)
         out, _ = _C().gemm(x, w, False, 0, None, None)
         for rows in (slice(0, 256), slice(M - 300, M)):
-            assert rel_err(out[rows], x[rows].float() @ w.float().t()) < 1e-2
+            within_bf16_budget("fwd rows", out[rows], x[rows].float() @ w.float().t(), x[rows] @ w.t())
     else:  # out (M, 128) = dl (M, V) W (V, 128)
         dl, w = _rnd(g, M, V), _rnd(g, V, 128)
         out, _ = _C().gemm(dl, w, True, 0, None, None)
         for rows in (slice(0, 256), slice(M - 300, M)):
-            assert rel_err(out[rows], dl[rows].float() @ w.float()) < 1e-2
+            within_bf16_budget("dgrad rows", out[rows], dl[rows].float() @ w.float(), dl[rows] @ w)
