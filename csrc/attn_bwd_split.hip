@@ -140,7 +140,14 @@ __host__ __device__ constexpr int kv_waves() { return 4; }
 // s_memtime deltas of the five phases of a query tile (S/dP chain issue, softmax, dV/dK
 // issue, LDS stage write, barrier) and writes them with its active-tile count and lifetime
 // over p.dq (the dQ kernel is then skipped): scripts/attn_stamps.py, profiles/attn_r03/.
-template <int D, bool CAUSAL, bool STAMPS = false>
+// PAIR: a workgroup takes key blocks kt and nkt - 1 - kt of one (batch, KV head) in turn, so
+// under the causal mask every workgroup has the same number of query tiles (nkt + 1 in all),
+// and the work ids are ordered (batch, head)-major through the XCD remap: the ~nkt / 2
+// workgroups of a (batch, head) run at once on one XCD and read its Q / dO tiles from that
+// XCD's L2.  Round 3 measured the (batch, head)-grouped order alone: per-tile load waits fell
+// 39 % but the kernels got slower -- heaviest-first ordering was lost and heavy blocks
+// finished last; pairing removes that tail.
+template <int D, bool CAUSAL, bool STAMPS = false, bool PAIR = false>
 __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
   constexpr int NW = kv_waves<D>(), NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
@@ -159,8 +166,22 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h32 = lane >> 5, l32 = lane & 31;
   const int BHk = p.B * p.Hkv;
-  const int kt = blockIdx.x / BHk;  // small kt = most work under the causal mask: first
-  const int bh = blockIdx.x % BHk;
+  const int nkt = (p.Tk + BNK - 1) / BNK;
+  int kt0_, npass = 1, bh;
+  if constexpr (PAIR) {
+    const int npair = (nkt + 1) / 2;
+    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int w = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    bh = w / npair;
+    kt0_ = w % npair;
+    npass = nkt - 1 - kt0_ != kt0_ ? 2 : 1;
+  } else {
+    kt0_ = blockIdx.x / BHk;  // small kt = most work under the causal mask: first
+    bh = blockIdx.x % BHk;
+  }
+#pragma nounroll
+  for (int pass = 0; pass < npass; ++pass) {
+  const int kt = __builtin_amdgcn_readfirstlane(pass == 0 ? kt0_ : nkt - 1 - kt0_);
   const int b = bh / p.Hkv, hk = bh % p.Hkv;
   const int rep = p.Hq / p.Hkv;
   const int kt0 = kt * BNK, kw0 = kt0 + wv * 32, mykey = kw0 + l32;
@@ -405,6 +426,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
         *reinterpret_cast<bf16x4*>(dVb + db * 32 + 8 * g4 + 4 * h32) = v4;
       }
   }
+  }  // pass
 }
 
 // ============================================================================ dQ
@@ -615,6 +637,23 @@ static void split_attrs() {
   }
 }
 
+template <int D, bool CAUSAL>
+static void kv_launch(const AttnParams& q, int grid, bool pair, hipStream_t st) {
+  if constexpr (CAUSAL) {
+    if (pair) {
+      static bool done = false;
+      if (!done) {
+        (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, true, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(D));
+        done = true;
+      }
+      attn_bwd_kv_kernel<D, true, false, true><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
+      return;
+    }
+  }
+  attn_bwd_kv_kernel<D, CAUSAL><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
+}
+
 template <bool CAUSAL>
 static void bias_attrs() {
   static bool done = false;
@@ -629,6 +668,17 @@ static void bias_attrs() {
 // separate delta pass.  Fused measured 0.3 % SLOWER end to end (1,004.2k vs 1,007.4k tok/s, four
 // alternating runs, profiles/ab/ab_attn_delta.log): the dQ kernel's extra O loads sit in its
 // prologue, ahead of the first K/V tile, which costs more than the 35 us HBM-bound pass.
+// ORION_ATTN_PAIR=0: the dK/dV kernel's one-key-block-per-workgroup, heaviest-first order
+// instead of the paired, (batch, head)-grouped one (attn_bwd_kv_kernel PAIR; causal only)
+static bool kv_pair() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORION_ATTN_PAIR");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 static bool delta_fused() {
   static int v = -1;
   if (v < 0) {
@@ -654,7 +704,9 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   const int pre_grid = (int)((rows * (D / 8) + 255) / 256);
   AttnParams q = p;
   q.delta = delta;
-  const int kv_grid = ((p.Tk + 32 * 4 - 1) / (32 * 4)) * p.B * p.Hkv;
+  const int nkt = (p.Tk + 32 * 4 - 1) / (32 * 4);
+  const bool pair = causal && kv_pair();
+  const int kv_grid = (pair ? (nkt + 1) / 2 : nkt) * p.B * p.Hkv;
   const int dq_grid = ((p.T + 127) / 128) * p.B * p.Hq;
   const bool fused = delta_fused();
   static const bool diag = getenv("ORION_ATTN_DIAG") && getenv("ORION_ATTN_DIAG")[0] == '1';
@@ -677,7 +729,7 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   split_attrs<64, CC>();                                                                            \
   bias_attrs<CC>();                                                                                 \
   attn_delta_kernel<64, true><<<pre_grid, 256, 0, st>>>(q, delta);                                  \
-  attn_bwd_kv_kernel<64, CC><<<kv_grid, kv_waves<64>() * 64, kv_lds(64), st>>>(q);                  \
+  kv_launch<64, CC>(q, kv_grid, pair, st);                                                          \
   attn_bwd_dq_kernel<64, CC, false, true><<<dq_grid, 256, dq_lds(64), st>>>(q);
     if (causal) { SPLITB(true) } else { SPLITB(false) }
 #undef SPLITB
@@ -687,10 +739,10 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   split_attrs<DD, CC>();                                                                \
   if (fused) {                                                                          \
     attn_bwd_dq_kernel<DD, CC, true><<<dq_grid, 256, dq_lds(DD), st>>>(q);              \
-    attn_bwd_kv_kernel<DD, CC><<<kv_grid, kv_waves<DD>() * 64, kv_lds(DD), st>>>(q);    \
+    kv_launch<DD, CC>(q, kv_grid, pair, st);                                            \
   } else {                                                                              \
     attn_delta_kernel<DD><<<pre_grid, 256, 0, st>>>(p, delta);                          \
-    attn_bwd_kv_kernel<DD, CC><<<kv_grid, kv_waves<DD>() * 64, kv_lds(DD), st>>>(q);    \
+    kv_launch<DD, CC>(q, kv_grid, pair, st);                                            \
     attn_bwd_dq_kernel<DD, CC, false><<<dq_grid, 256, dq_lds(DD), st>>>(q);             \
   }
   if (D == 64) {

@@ -569,6 +569,33 @@ std::tuple<Tensor, Tensor> gemm_gelu_bwd(const Tensor& dy, const Tensor& w, cons
   return {out.view(sizes), given ? Tensor() : db};
 }
 
+// dgate_up = SwiGLU'(gate_up) applied to dy . w: the fused backward of silu(gate) * up ->
+// linear (Llama's down_proj), one in-tree GEMM (K = model dim, N = ffn dim) whose epilogue
+// reads the packed (M, 2F) [gate | up] forward projection and writes the packed (M, 2F)
+// gradient: the (M, F) input gradient of the SwiGLU is never written and re-read.
+Tensor gemm_swiglu_bwd(const Tensor& dy, const Tensor& w, const Tensor& gate_up) {
+  check_bf16(dy, "dy");
+  check_bf16(w, "w");
+  check_bf16(gate_up, "gate_up");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemm_swiglu_bwd: w must be a contiguous (K, F)");
+  const int64_t K = w.size(0), F = w.size(1);
+  TORCH_CHECK(dy.size(-1) == K, "gemm_swiglu_bwd: dy (..., K)");
+  auto x2 = dy.reshape({-1, K});
+  TORCH_CHECK(x2.stride(1) == 1, "gemm_swiglu_bwd: dy must flatten to rows");
+  const int64_t M = x2.size(0);
+  auto gu = gate_up.reshape({-1, 2 * F});
+  TORCH_CHECK(gu.size(0) == M && gu.stride(1) == 1, "gemm_swiglu_bwd: gate_up must be (M, 2F)");
+  TORCH_CHECK(M < (1LL << 31) && F < (1 << 29), "gemm_swiglu_bwd: shape too large");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  auto out = at::empty({M, 2 * F}, dy.options());
+  char* o = static_cast<char*>(out.data_ptr());
+  check_launch(orion_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), (int)M, (int)F, (int)K, 1,
+                          5, o, 2 * F, nullptr, o + F * 2, 2 * F, gu.data_ptr(), gu.stride(0), cur_stream()),
+               "gemm_swiglu_bwd");
+  auto sizes = gate_up.sizes().vec();
+  return out.view(sizes);
+}
+
 // ------------------------------------------------------------------ optimizer
 void grad_sumsq(const Tensor& g, Tensor out) {
   check_grad_out(g, "grads");
@@ -873,6 +900,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");
+  m.def("gemm_swiglu_bwd(Tensor dy, Tensor w, Tensor gate_up) -> Tensor");
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
@@ -903,6 +931,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
   m.impl("gemm", &gemm);
   m.impl("gemm_gelu_bwd", &gemm_gelu_bwd);
+  m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
   m.impl("grad_sumsq", &grad_sumsq);
   m.impl("adamw_flat", &adamw_flat);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);

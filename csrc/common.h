@@ -154,6 +154,13 @@ ORION_DEVICE f32x2 gelu_grad_x2(f32x2 x) {
 
 ORION_DEVICE float silu_f(float x) { return x / (1.f + __expf(-x)); }
 
+// sigmoid of a pair: 1 / (1 + 2^(-x log2 e)), one v_exp_f32 + one v_rcp_f32 per value
+ORION_DEVICE f32x2 sigmoid2(f32x2 x) {
+  const f32x2 z = x * splat2(-1.4426950408889634f);
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + splat2(1.f);
+  return f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
 }  // namespace orion
 
 #define HIP_LAUNCH_CHECK() (void)hipGetLastError()

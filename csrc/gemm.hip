@@ -11,6 +11,8 @@
 //   EPI_BIAS_GELU  out = a = acc + bias[n], out2 = gelu_tanh(a)              (MLP c_fc)
 //   EPI_GELU_BWD   out = acc * gelu_tanh'(pre[m][n] [+ bias[n]]), optional   (MLP c_proj dgrad)
 //                  per-64-row column sums of out (the fc bias gradient)
+//   EPI_SWIGLU_BWD out = acc * up * silu'(gate), out2 = acc * silu(gate)     (Llama down_proj
+//                  with gate = pre[m][n], up = pre[m][N + n]                   dgrad)
 // The last two remove the separate bias+GELU forward and GELU backward HBM passes over the
 // (tokens x 4C) activation.
 //
@@ -30,8 +32,9 @@ int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int 
 
 // Diagnostic flags (GemmArgs::flags): 4 = gemm16's stamped instantiation (EPI_STORE, the
 // stamp buffer passed as `pre`), 32 = with its stores waited for, 64 = one workgroup per work
-// item instead of the persistent walk.  Read once from ORION_GEMM_DIAG; scripts change them
-// in-process through orion_gemm_set_diag (the gemm_diag op).
+// item instead of the persistent walk, bits 8-15 = the m-tile group size of the work order.
+// Read once from ORION_GEMM_DIAG; scripts change them in-process through orion_gemm_set_diag
+// (the gemm_diag op).
 static int g_diag = -1;
 
 static int gemm_diag() {
@@ -66,7 +69,9 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
        reinterpret_cast<uintptr_t>(out)) & 15) return -2;
   if ((epi == EPI_BIAS || epi == EPI_BIAS_GELU) && !bias) return -3;
   if (epi == EPI_BIAS_GELU && (!out2 || ldo2 % 8 || (reinterpret_cast<uintptr_t>(out2) & 15))) return -3;
-  if (epi == EPI_GELU_BWD && (!pre || ldp % 8 || (reinterpret_cast<uintptr_t>(pre) & 15))) return -3;
+  if ((epi == EPI_GELU_BWD || epi == EPI_SWIGLU_BWD) && (!pre || ldp % 8 || (reinterpret_cast<uintptr_t>(pre) & 15)))
+    return -3;
+  if (epi == EPI_SWIGLU_BWD && (!wkm || !out2 || ldo2 % 8 || (reinterpret_cast<uintptr_t>(out2) & 15))) return -3;
   if (db && (epi != EPI_GELU_BWD || !part || ldo != N)) return -3;
   GemmArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)out, ldo,
              (const bf16_t*)bias, (bf16_t*)out2, ldo2, (const bf16_t*)pre, ldp,

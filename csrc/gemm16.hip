@@ -63,8 +63,9 @@ struct G16Item {
 
 ORION_DEVICE G16Item g16_decode(const GemmArgs& g, int w) {
   // k chunk, then groups of GM m-tiles with the m-tile fastest (the ~32 tiles an XCD runs at
-  // once share GM X panels and ~32 / GM W panels in its L2)
-  constexpr int GM = 4;
+  // once share GM X panels and ~32 / GM W panels in its L2); flags bits 8-15 override GM
+  // (diagnostic sweep)
+  const int GM = (g.flags >> 8) & 0xFF ? (g.flags >> 8) & 0xFF : 4;
   const int tiles_m = (g.M + 255) >> 8, tiles = tiles_m * g.tiles_n;
   G16Item it;
   it.kc = w / tiles;
@@ -128,7 +129,7 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
   const __amdgpu_buffer_rsrc_t ro =
       make_rsrc(g.out + (long)m0 * g.ldo, (unsigned)(((long)(rows_m - 1) * g.ldo + g.N) * 2));
   [[maybe_unused]] __amdgpu_buffer_rsrc_t ro2 = ro;
-  if constexpr (EPI == EPI_BIAS_GELU)
+  if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD)
     ro2 = make_rsrc(g.out2 + (long)m0 * g.ldo2, (unsigned)(((long)(rows_m - 1) * g.ldo2 + g.N) * 2));
   constexpr bool CS = EPI == EPI_GELU_BWD;
   // bf16 pair word -> two floats (low half first)
@@ -147,20 +148,28 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       else bias4[ap] = u32x4{0u, 0u, 0u, 0u};
     }
   }
-  [[maybe_unused]] u32x4 pre4[4][4];
-  if constexpr (EPI == EPI_GELU_BWD) {
-    const __amdgpu_buffer_rsrc_t rp =
-        make_rsrc(g.pre + (long)m0 * g.ldp, (unsigned)(((long)(rows_m - 1) * g.ldp + g.N) * 2));
+  // GELU' / SwiGLU' operands (the pre-activation, or the gate and up halves of the packed
+  // gate_up projection) stream in one column group (ap) ahead of their use: the loads of group
+  // ap + 1 are issued before the stores of group ap, so waiting for them never waits for those
+  // stores, and only two groups' operands are live (32 / 64 VGPRs instead of 64 / 128)
+  constexpr bool PRE = EPI == EPI_GELU_BWD || EPI == EPI_SWIGLU_BWD;
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t rp;
+  if constexpr (PRE)
+    rp = make_rsrc(g.pre + (long)m0 * g.ldp,
+                   (unsigned)(((long)(rows_m - 1) * g.ldp + (EPI == EPI_SWIGLU_BWD ? 2 : 1) * g.N) * 2));
+  auto load_pre = [&](int ap, u32x4 (&pa)[4], u32x4 (&pb)[4]) {
+    const int nb = ncol(ap), nc = nb < g.N ? nb : 0;
 #pragma unroll
-    for (int ap = 0; ap < 4; ++ap) {
-      const int nb = ncol(ap), nc = nb < g.N ? nb : 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int mc = min(mw + 16 * b + i16, g.M - 1);
-        pre4[ap][b] = __builtin_amdgcn_raw_buffer_load_b128(rp, (unsigned)(((long)(mc - m0) * g.ldp + nc) * 2), 0, 0);
-      }
+    for (int b = 0; b < 4; ++b) {
+      const int mc = min(mw + 16 * b + i16, g.M - 1);
+      const unsigned o = (unsigned)(((long)(mc - m0) * g.ldp + nc) * 2);
+      pa[b] = __builtin_amdgcn_raw_buffer_load_b128(rp, o, 0, 0);
+      if constexpr (EPI == EPI_SWIGLU_BWD)  // up half: F columns further
+        pb[b] = __builtin_amdgcn_raw_buffer_load_b128(rp, o + (unsigned)g.N * 2, 0, 0);
     }
-  }
+  };
+  [[maybe_unused]] u32x4 preA[4], preB[4], upA[4], upB[4];
+  if constexpr (PRE) load_pre(0, preA, upA);
   // the value arithmetic runs on pairs of adjacent columns (v_pk_*_f32: no MFMA issues beside
   // the epilogue) and every pair is packed to bf16 by one v_cvt_pk_bf16_f32
 #pragma unroll
@@ -168,6 +177,12 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
     // after the swap: lane (q, i16) holds n = nb .. nb + 7 of row m (fp32)
     const int nb = ncol(ap);
     const bool nok = nb < g.N;
+    if constexpr (PRE) {
+      if (ap + 1 < 4) {
+        if (ap & 1) load_pre(ap + 1, preA, upA);
+        else load_pre(ap + 1, preB, upB);
+      }
+    }
     [[maybe_unused]] f32x2 bias[4];
     if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_GELU_BWD) {
 #pragma unroll
@@ -177,8 +192,11 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int m = mw + 16 * b + i16;
-      [[maybe_unused]] u32x4 p4;
-      if constexpr (EPI == EPI_GELU_BWD) p4 = pre4[ap][b];
+      [[maybe_unused]] u32x4 p4, u4;
+      if constexpr (PRE) {
+        p4 = (ap & 1) ? preB[b] : preA[b];
+        u4 = (ap & 1) ? upB[b] : upA[b];
+      }
       f32x2 v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -195,16 +213,30 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] *= gelu_grad_x2(unpack2(p4[e]) + bias[e]);
       }
+      [[maybe_unused]] f32x2 du[4];
+      if constexpr (EPI == EPI_SWIGLU_BWD) {
+        // v = dh; dgate = dh u silu'(g), dup = dh silu(g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x2 gg = unpack2(p4[e]), uu = unpack2(u4[e]);
+          const f32x2 sg = sigmoid2(gg);
+          du[e] = v[e] * gg * sg;
+          v[e] = v[e] * uu * fma2(gg * sg, splat2(1.f) - sg, sg);
+        }
+      }
       const bool ok = m < g.M && nok;
       const unsigned off = ok ? (unsigned)(((long)(m - m0) * g.ldo + nb) * 2) : 0xFFFFFFF0u;
       u32x4 pk;
 #pragma unroll
       for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(v[e]);
       __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, 0);
-      if constexpr (EPI == EPI_BIAS_GELU) {
+      if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
         const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(gelu_x2(v[e]));
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (EPI == EPI_BIAS_GELU) pk[e] = pack2_bf16(gelu_x2(v[e]));
+          else pk[e] = pack2_bf16(du[e]);
+        }
         __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off2, 0, 0);
       }
       if constexpr (CS) {
@@ -373,26 +405,32 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
 #pragma unroll
     for (int e = 0; e < 2; ++e) blds16(rw, vo[p][e], (unsigned)tw * wstep, base + ld[p][e]);
   };
+  // A stream that has issued its last k-tile stays on it: the DMA of the final one or two
+  // steps re-loads that tile into a buffer no phase reads any more, so every phase issues the
+  // same pieces and waits the same count (no branches in the steady state); the kernel drains
+  // them (vmcnt(0)) before it ends.
   auto advance_x = [&]() {
     ++sx;
-    if (++tx == nkx) {
+    if (tx + 1 < nkx) {
+      ++tx;
+    } else if (jx + 1 < nitems) {
+      ++jx;
       tx = 0;
-      if (++jx < nitems) {
-        const G16Item it = g16_decode(g, item_id(jx));
-        setup_x(it);
-        nkx = it.nk;
-      }
+      const G16Item it = g16_decode(g, item_id(jx));
+      setup_x(it);
+      nkx = it.nk;
     }
   };
   auto advance_w = [&]() {
     ++sw;
-    if (++tw == nkw) {
+    if (tw + 1 < nkw) {
+      ++tw;
+    } else if (jw + 1 < nitems) {
+      ++jw;
       tw = 0;
-      if (++jw < nitems) {
-        const G16Item it = g16_decode(g, item_id(jw));
-        setup_w(it);
-        nkw = it.nk;
-      }
+      const G16Item it = g16_decode(g, item_id(jw));
+      setup_w(it);
+      nkw = it.nk;
     }
   };
 
@@ -469,7 +507,6 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   // before the next phase), MMA slot (32 MFMAs)
   auto phase = [&](auto Hc, int s, int t) {
     constexpr int H = decltype(Hc)::value;
-    const bool isw = jw < nitems, isx = jx < nitems;
     stamp(t, 2 + 6 * H);
     if constexpr (H == 0) {
       read_w(W0, s, Hc);
@@ -478,12 +515,10 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
     } else {
       read_w(W1, s, Hc);
     }
-    if (isw) issue_w(H);
-    if (isx) issue_x(H);
+    issue_w(H);
+    issue_x(H);
     stamp(t, 3 + 6 * H);
-    if (isw && isx) wait_vm_exact<4>();
-    else if (isw || isx) wait_vm_exact<2>();
-    else wait_vm_exact<0>();
+    wait_vm_exact<4>();
     stamp(t, 4 + 6 * H);
     g_barrier();
     stamp(t, 5 + 6 * H);
@@ -520,13 +555,17 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   issue_w(0);
   issue_w(1);
   advance_w();
-  if (jx < nitems) {
-    issue_x(0);
-    issue_x(1);
-    advance_x();
-    wait_vm_exact<6>();
-  } else {
-    wait_vm_exact<2>();
+  issue_x(0);
+  issue_x(1);
+  advance_x();
+  wait_vm_exact<6>();
+  if ((g.flags & 128) && nitems > 1 && (lcl & 1)) {
+    // stagger (flags & 128): every other workgroup of an XCD starts half an item late, so
+    // the chip's epilogue store bursts alternate between two halves of the CUs instead of
+    // all 256 storing at once (the epilogue is store-bandwidth-bound when they do)
+    const unsigned long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long delay = (unsigned long)nkx * 1400;  // ~half of a k-tile's 2,800 cycles
+    while (__builtin_amdgcn_s_memtime() - t0 < delay) __builtin_amdgcn_s_sleep(8);
   }
   if constexpr (STAMPS) stp[1] = __builtin_amdgcn_s_memtime();
   g_barrier();
@@ -543,13 +582,14 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
     for (int t = 0; t < it.nk; ++t, ++s) {
       phase(I0(), s, t);
       phase(I1(), s, t);
-      if (jw < nitems) advance_w();
-      if (jx < nitems) advance_x();
+      advance_w();
+      advance_x();
     }
     if constexpr (STAMPS) stp[14] = __builtin_amdgcn_s_memtime();
     g16_epilogue<EPI>(g, acc, it, wm, grp, q, i16);
   }
   if (grp == 0) g_barrier();  // match group 1's barrier count
+  wait_vm_exact<0>();         // the stream's last (dummy) LDS-DMA lands before the LDS is freed
   if constexpr (STAMPS) {
     // 15: epilogue issued; 16: where the wave ran (HW_ID: cu / sh / se; XCC_ID); 17: its
     // stores acknowledged (only with flags & 32, which waits for them: the default leaves the
@@ -616,6 +656,7 @@ int gemm16(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
     case EPI_BIAS * 2 + 0: return gemm16_launch<false, false, EPI_BIAS>(a, st);
     case EPI_BIAS_GELU * 2 + 0: return gemm16_launch<false, false, EPI_BIAS_GELU>(a, st);
     case EPI_GELU_BWD * 2 + 1: return gemm16_launch<false, true, EPI_GELU_BWD>(a, st);
+    case EPI_SWIGLU_BWD * 2 + 1: return gemm16_launch<false, true, EPI_SWIGLU_BWD>(a, st);
     default: return -4;
   }
 }

@@ -6,7 +6,8 @@
 
 namespace orion {
 
-enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3, EPI_WGRAD = 4 };
+enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3, EPI_WGRAD = 4,
+               EPI_SWIGLU_BWD = 5 };
 
 struct GemmArgs {
   const bf16_t* X;  long ldx;   // [M][K] row-major
@@ -14,10 +15,12 @@ struct GemmArgs {
   bf16_t* out;      long ldo;   // [M][N]
   const bf16_t* bias;           // [N]                      (EPI_BIAS, EPI_BIAS_GELU)
   bf16_t* out2;     long ldo2;  // gelu(a), [M][N]          (EPI_BIAS_GELU)
-  const bf16_t* pre; long ldp;  // pre-activation a, [M][N] (EPI_GELU_BWD)
+  const bf16_t* pre; long ldp;  // pre-activation a, [M][N] (EPI_GELU_BWD); the packed [M][2N]
+                                // gate | up projection (EPI_SWIGLU_BWD: out = dgate, out2 = dup)
   int M, N, K, tiles_n;
   int flags;  // diagnostics (ORION_GEMM_DIAG, csrc/gemm.hip): 4 = stamped instantiation,
-              // 32 = + stores waited for, 64 = one workgroup per work item (no persistent walk)
+              // 32 = + stores waited for, 64 = one workgroup per work item (no persistent walk),
+              // bits 8-15: m-tile group size of the work order (0 = 4)
   // split-K (EPI_WGRAD): work item = (k chunk of kchunk rows, tile)
   int kchunk, ksplit;
   float* slabs;          // ksplit > 1: fp32 partial tiles [ksplit][M][N]

@@ -89,7 +89,7 @@ class FeedForward(nn.Module):
         self.down_proj = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)
 
     def forward(self, x):
-        return ops.linear(ops.swiglu(ops.linear(x, self.gate_up_proj.weight)), self.down_proj.weight)
+        return ops.swiglu_mlp(x, self.gate_up_proj.weight, self.down_proj.weight)
 
 
 class DecoderLayer(nn.Module):

@@ -145,6 +145,18 @@ def mlp(x, w_fc, b_fc, w_proj, b_proj=None):
     return gelu_linear(linear(x, w_fc), b_fc, w_proj, b_proj)
 
 
+def swiglu_mlp(x, w_gate_up, w_down):
+    """Llama's feed-forward: linear(swiglu(x W_gu^T), W_down) with W_gu = [W_gate; W_up].  On
+    the GPU path the SwiGLU backward runs in the down_proj input-gradient GEMM's epilogue
+    (ops/activations.py ``_SwigluMLP``)."""
+    b = _gpu(x)
+    if b == "hip":
+        from .activations import swiglu_mlp_hip, swiglu_mlp_ok
+        if swiglu_mlp_ok(x, w_gate_up, w_down):
+            return swiglu_mlp_hip(x, w_gate_up, w_down)
+    return linear(swiglu(linear(x, w_gate_up)), w_down)
+
+
 def swiglu(gate_up):
     """silu(gate) * up on a packed (..., 2F) [gate | up] projection -> (..., F)."""
     b = _gpu(gate_up)
@@ -267,7 +279,7 @@ def linear_cross_entropy(x, weight, targets, ignore_index=-1):
 __all__ = [
     "set_backend", "backend", "ext_available", "load_ext",
     "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm", "rope",
-    "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy",
+    "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "swiglu_mlp",
     "linear_cross_entropy",
 ]
 
@@ -315,7 +327,7 @@ def _guarded(fn):
 
 
 for _name in ("layer_norm", "add_layer_norm", "add_rms_norm", "linear", "rms_norm", "bias_gelu",
-              "gelu_linear", "mlp", "embed_layer_norm", "add_broadcast", "linear_attention_qkv",
+              "gelu_linear", "mlp", "swiglu_mlp", "embed_layer_norm", "add_broadcast", "linear_attention_qkv",
               "linear_cross_entropy"):
     globals()[_name] = _guarded(globals()[_name])
 del _name

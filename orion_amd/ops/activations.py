@@ -205,3 +205,72 @@ class _FusedMLP(torch.autograd.Function):
 
 def mlp_hip(x, w_fc, b_fc, w_proj, b_proj=None):
     return _FusedMLP.apply(x, w_fc, b_fc, w_proj, b_proj)
+
+
+# ORION_FUSED_SWIGLU=1 (default): Llama's feed-forward with the SwiGLU backward inside the
+# down_proj input-gradient GEMM's epilogue (csrc/gemm16.hip EPI_SWIGLU_BWD): per layer the
+# (M, F) gradient of the SwiGLU output is never written and re-read, and the separate
+# swiglu_bwd pass over (M, 2F) is gone.
+_FUSED_SWIGLU = os.environ.get("ORION_FUSED_SWIGLU", "1") != "0"
+
+
+def swiglu_mlp_ok(x, w_gu, w_down) -> bool:
+    from .gemm import gemm16_addressable
+    C_, F2 = x.shape[-1], w_gu.shape[0]
+    F_ = F2 // 2
+    return (_FUSED_SWIGLU and x.dtype == torch.bfloat16 and w_gu.dtype == torch.bfloat16
+            and w_down.dtype == torch.bfloat16 and x.is_contiguous() and w_gu.is_contiguous()
+            and w_down.is_contiguous() and F2 % 2 == 0 and w_down.shape == (C_, F_)
+            and C_ % 64 == 0 and F_ % 8 == 0 and x.data_ptr() % 16 == 0
+            and w_gu.data_ptr() % 16 == 0 and w_down.data_ptr() % 16 == 0
+            and gemm16_addressable(C_, C_, F_, True) and gemm16_addressable(2 * F_, 2 * F_, F_, False))
+
+
+class _SwigluMLP(torch.autograd.Function):
+    """y = (silu(x W_g^T) * (x W_u^T)) W_down^T with W_gu = [W_g; W_u] packed, Llama's
+    feed-forward.
+
+    forward   gu = x W_gu^T (hipBLASLt), h = swiglu(gu) (csrc/activations.hip), y = h W_down^T;
+    backward  dgu = ONE in-tree GEMM dy W_down whose epilogue reads gate / up from gu and
+              writes dgate = dh up silu'(gate), dup = dh silu(gate) straight into the packed
+              (M, 2F) gradient; dW_down = dy^T h, dx = dgu W_gu, dW_gu = dgu^T x (weight
+              gradients straight into the arena)."""
+
+    @staticmethod
+    def forward(ctx, x, w_gu, w_down):
+        C_ = x.shape[-1]
+        x2 = x.reshape(-1, C_)
+        gu = linear_fwd(x2, w_gu)
+        h = C().swiglu_fwd(gu)
+        y = linear_fwd(h, w_down)
+        ctx.save_for_backward(x2, gu, h, w_gu, w_down)
+        ctx.sinks = (sink_of(w_gu), sink_of(w_down))
+        ctx.x_shape = x.shape
+        return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gu, h, w_gu, w_down = ctx.saved_tensors
+        s_gu, s_down = ctx.sinks
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dgu = C().gemm_swiglu_bwd(dy2, w_down, gu)
+        grads = [None, None, None]
+        if ctx.needs_input_grad[2]:
+            if s_down is not None:
+                wgrad_into(dy2, h, s_down.view, s_down.take())
+                s_down.notify()
+            else:
+                grads[2] = wgrad(dy2, h)
+        if ctx.needs_input_grad[0]:
+            grads[0] = linear_dgrad(dgu, w_gu).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            if s_gu is not None:
+                wgrad_into(dgu, x2, s_gu.view, s_gu.take())
+                s_gu.notify()
+            else:
+                grads[1] = wgrad(dgu, x2)
+        return tuple(grads)
+
+
+def swiglu_mlp_hip(x, w_gu, w_down):
+    return _SwigluMLP.apply(x, w_gu, w_down)

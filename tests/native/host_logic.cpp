@@ -65,6 +65,9 @@ int main() {
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 0, 2, o, 64, p, nullptr, 64, nullptr, 0, 0) == -3);        // gelu out2 missing
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 3, o, 64, nullptr, nullptr, 0, nullptr, 0, 0) == -3);   // pre missing
   CHECK(orion_gemm(p, 64, p, 64, 0, 64, 64, 0, 0, o, 64, nullptr, nullptr, 0, nullptr, 0, 0) == -1);    // M = 0
+  CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 0, 5, o, 128, nullptr, o, 128, p, 128, 0) == -3);         // swiglu: NN only
+  CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 5, o, 128, nullptr, nullptr, 0, p, 128, 0) == -3);     // swiglu: out2 missing
+  CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 5, o, 128, nullptr, o, 128, nullptr, 0, 0) == -3);     // swiglu: pre missing
   float part[4096];
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 0, o, 64, nullptr, nullptr, 0, nullptr, 0, 0, o, 0, part) == -3);  // db needs epi 3
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 3, o, 64, nullptr, nullptr, 0, p, 64, 0, o, 0, nullptr) == -3);  // db needs scratch

@@ -215,3 +215,45 @@ def test_gemm16_operands_past_4gb(wkm, monkeypatch):
         out, _ = _C().gemm(dl, w, True, 0, None, None)
         for rows in (slice(0, 256), slice(M - 300, M)):
             within_bf16_budget("dgrad rows", out[rows], dl[rows].float() @ w.float(), dl[rows] @ w)
+
+
+@pytest.mark.parametrize("M,C_,F_", [(333, 256, 512), (4096, 1024, 2752), (1000, 512, 1376)])
+def test_gemm_swiglu_bwd_epilogue(M, C_, F_, gemm_cfg):
+    """gemm_swiglu_bwd: dh = dy W_down (W_down (C, F) read k-major) with the SwiGLU backward in
+    the epilogue: dgate = dh up silu'(gate), dup = dh silu(gate) into the packed (M, 2F)."""
+    g = torch.Generator(device=DEV).manual_seed(M + F_)
+    dy, w, gu = _rnd(g, M, C_), _rnd(g, C_, F_), _rnd(g, M, 2 * F_)
+    got = _C().gemm_swiglu_bwd(dy, w, gu)
+    gr = gu.float().requires_grad_()
+    ga, ua = gr.chunk(2, -1)
+    (torch.nn.functional.silu(ga) * ua).backward(dy.float() @ w.float())
+    gb = gu.clone().requires_grad_()
+    a_, b_ = gb.chunk(2, -1)
+    (torch.nn.functional.silu(a_) * b_).backward(dy @ w)
+    assert got.shape == (M, 2 * F_)
+    within_bf16_budget("dgate", got[:, :F_], gr.grad[:, :F_], gb.grad[:, :F_])
+    within_bf16_budget("dup", got[:, F_:], gr.grad[:, F_:], gb.grad[:, F_:])
+
+
+def test_swiglu_mlp_matches_reference():
+    """ops.swiglu_mlp (Llama feed-forward, SwiGLU backward fused into the down_proj input
+    gradient GEMM) against fp32 autograd: output and every gradient, ragged token count."""
+    from orion_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = _rnd(g, 3, 111, 512)
+    wgu, wd = _rnd(g, 2 * 1376, 512) * 0.1, _rnd(g, 512, 1376) * 0.05
+    dy = _rnd(g, 3, 111, 512)
+    ts = [t.clone().requires_grad_() for t in (x, wgu, wd)]
+    y = ops.swiglu_mlp(*ts)
+    y.backward(dy)
+    fs = [t.detach().float().requires_grad_() for t in (x, wgu, wd)]
+    ga, ua = (fs[0] @ fs[1].t()).chunk(2, -1)
+    yr = (torch.nn.functional.silu(ga) * ua) @ fs[2].t()
+    yr.backward(dy.float())
+    bs = [t.detach().clone().requires_grad_() for t in (x, wgu, wd)]
+    gb_, ub_ = (bs[0] @ bs[1].t()).chunk(2, -1)
+    yb = (torch.nn.functional.silu(gb_) * ub_) @ bs[2].t()
+    yb.backward(dy)
+    within_bf16_budget("y", y, yr, yb)
+    for n, t, f, b in zip(("dx", "dwgu", "dwdown"), ts, fs, bs):
+        within_bf16_budget(n, t.grad, f.grad, b.grad)

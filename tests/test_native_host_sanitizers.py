@@ -9,8 +9,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
-SOURCES = ["tests/native/host_logic.cpp", "csrc/gemm.hip", "csrc/gemm_phased.hip", "csrc/gemm16.hip",
-           "csrc/wgrad.hip",
+SOURCES = ["tests/native/host_logic.cpp", "csrc/gemm.hip", "csrc/gemm16.hip", "csrc/wgrad.hip",
            "csrc/layernorm.hip", "csrc/rmsnorm_rope.hip", "csrc/activations.hip"]
 
 

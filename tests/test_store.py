@@ -163,6 +163,9 @@ def test_sqlite_reservation_is_constant_time(tmp_path):
     import statistics
     small, small_cas = _reservation_times(tmp_path / "small.sqlite", 100)
     big, big_cas = _reservation_times(tmp_path / "big.sqlite", 10**4)
-    # a parse of every pending trial would make the 10^4 case ~100x the 100 case
-    assert statistics.median(big) < 3 * statistics.median(small) + 0.002, (big, small)
+    # a parse of every pending trial would make the 10^4 case ~100x the 100 case -- in every
+    # sample, so the fastest samples are compared (the median drifts with disk/CPU contention
+    # from parallel test workers)
+    assert min(big) < 3 * min(small) + 0.002, (big, small)
+    assert statistics.median(big) < 20 * statistics.median(small) + 0.01, (big, small)
     assert big_cas < 3 * small_cas + 0.002, (big_cas, small_cas)
