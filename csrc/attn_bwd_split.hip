@@ -140,16 +140,12 @@ __host__ __device__ constexpr int kv_waves() { return 4; }
 // s_memtime deltas of the five phases of a query tile (S/dP chain issue, softmax, dV/dK
 // issue, LDS stage write, barrier) and writes them with its active-tile count and lifetime
 // over p.dq (the dQ kernel is then skipped): scripts/attn_stamps.py, profiles/attn_r03/.
-// PAIR: a workgroup takes key blocks kt and nkt - 1 - kt of one (batch, KV head) in turn, so
-// under the causal mask every workgroup has the same number of query tiles (nkt + 1 in all),
-// and the work ids are ordered (batch, head)-major through the XCD remap: the ~nkt / 2
-// workgroups of a (batch, head) run at once on one XCD and read its Q / dO tiles from that
-// XCD's L2.  Round 3 measured the (batch, head)-grouped order alone: per-tile load waits fell
-// 39 % but the kernels got slower -- heaviest-first ordering was lost and heavy blocks
-// finished last; pairing removes that tail.
-template <int D, bool CAUSAL, bool STAMPS = false, bool PAIR = false>
-__global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
-  constexpr int NW = kv_waves<D>(), NT = NW * 64;
+// NW: waves (32 keys each) per workgroup.  8 (256 keys, one workgroup of two waves per SIMD
+// per CU) halves the Q / dO bytes streamed from L2 per MFMA against 4 (128 keys, two or
+// three 4-wave workgroups per CU).
+template <int D, bool CAUSAL, bool STAMPS = false, int NW = kv_waves<D>()>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_bwd_kv_kernel(AttnParams p) {
+  constexpr int NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
   constexpr int QT = BMQ * D;            // Q / dO tile elements
   constexpr int NQC = BMQ * NCH;         // 16-byte chunks per Q (or dO) tile
@@ -166,22 +162,8 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h32 = lane >> 5, l32 = lane & 31;
   const int BHk = p.B * p.Hkv;
-  const int nkt = (p.Tk + BNK - 1) / BNK;
-  int kt0_, npass = 1, bh;
-  if constexpr (PAIR) {
-    const int npair = (nkt + 1) / 2;
-    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int w = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-    bh = w / npair;
-    kt0_ = w % npair;
-    npass = nkt - 1 - kt0_ != kt0_ ? 2 : 1;
-  } else {
-    kt0_ = blockIdx.x / BHk;  // small kt = most work under the causal mask: first
-    bh = blockIdx.x % BHk;
-  }
-#pragma nounroll
-  for (int pass = 0; pass < npass; ++pass) {
-  const int kt = __builtin_amdgcn_readfirstlane(pass == 0 ? kt0_ : nkt - 1 - kt0_);
+  const int kt = blockIdx.x / BHk;  // small kt = most work under the causal mask: first
+  const int bh = blockIdx.x % BHk;
   const int b = bh / p.Hkv, hk = bh % p.Hkv;
   const int rep = p.Hq / p.Hkv;
   const int kt0 = kt * BNK, kw0 = kt0 + wv * 32, mykey = kw0 + l32;
@@ -306,6 +288,13 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
     advance(nh, nq);
     swrite(0);
   }
+  // Retire the K / V fragment loads (and the prologue's) with a wait the compiler's wait-count
+  // pass can see on every path.  Without it the pass, merging the total == 0 path at the
+  // loop, left vmcnt waits for kf / vf in front of the S / dP MFMAs of EVERY step -- and in
+  // the steady state those counted waits drained the next step's Q / dO prefetch, so each
+  // step's MFMA chain sat out the full load latency (round 3's stamps: ~1,290 cycles in the
+  // S / dP chain, ~1,760 at the stage write).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_prev = 0, st_begin = 0;
   int st_n = 0;
@@ -426,7 +415,6 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
         *reinterpret_cast<bf16x4*>(dVb + db * 32 + 8 * g4 + 4 * h32) = v4;
       }
   }
-  }  // pass
 }
 
 // ============================================================================ dQ
@@ -623,62 +611,52 @@ static size_t kv_lds(int D) {
 }
 static size_t dq_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
 
-template <int D, bool CAUSAL>
-static void split_attrs() {
-  static bool done = false;
-  if (!done) {
-    hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, CAUSAL>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(D));
-    hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, false>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
-    hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, true>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
-    done = true;
+// ORION_ATTN_KV_NW=8: 8-wave (256-key) dK/dV workgroups at D = 64 (attn_bwd_kv_kernel NW)
+static int kv_nw() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORION_ATTN_KV_NW");
+    v = (e && atoi(e) == 8) ? 8 : 4;
   }
+  return v;
 }
 
-template <int D, bool CAUSAL>
-static void kv_launch(const AttnParams& q, int grid, bool pair, hipStream_t st) {
-  if constexpr (CAUSAL) {
-    if (pair) {
-      static bool done = false;
-      if (!done) {
-        (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, true, false, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(D));
-        done = true;
-      }
-      attn_bwd_kv_kernel<D, true, false, true><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
-      return;
-    }
-  }
-  attn_bwd_kv_kernel<D, CAUSAL><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
-}
-
-template <bool CAUSAL>
-static void bias_attrs() {
+template <int D, bool CAUSAL, int NW>
+static void kv_launch_nw(const AttnParams& q, hipStream_t st) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<64, CAUSAL, false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(64));
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, CAUSAL, false, NW>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(D));
     done = true;
   }
+  const int grid = ((q.Tk + 32 * NW - 1) / (32 * NW)) * q.B * q.Hkv;
+  attn_bwd_kv_kernel<D, CAUSAL, false, NW><<<grid, NW * 64, kv_lds(D), st>>>(q);
+}
+
+// D = 128 keeps 4 waves (its K fragments come from an LDS image sized for 128 keys)
+template <int D, bool CAUSAL>
+static void kv_launch(const AttnParams& q, int, hipStream_t st) {
+  if (D == 64 && kv_nw() == 8)
+    kv_launch_nw<D, CAUSAL, D == 64 ? 8 : 4>(q, st);
+  else
+    kv_launch_nw<D, CAUSAL, 4>(q, st);
+}
+
+template <int D, bool CAUSAL, bool FUSE, bool BIAS = false>
+static void dq_launch(const AttnParams& q, int grid, hipStream_t st) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, FUSE, BIAS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
+    done = true;
+  }
+  attn_bwd_dq_kernel<D, CAUSAL, FUSE, BIAS><<<grid, 256, dq_lds(D), st>>>(q);
 }
 
 // ORION_ATTN_DELTA=fused: delta computed inside the dQ kernel (launched first); default: the
 // separate delta pass.  Fused measured 0.3 % SLOWER end to end (1,004.2k vs 1,007.4k tok/s, four
 // alternating runs, profiles/ab/ab_attn_delta.log): the dQ kernel's extra O loads sit in its
 // prologue, ahead of the first K/V tile, which costs more than the 35 us HBM-bound pass.
-// ORION_ATTN_PAIR=0: the dK/dV kernel's one-key-block-per-workgroup, heaviest-first order
-// instead of the paired, (batch, head)-grouped one (attn_bwd_kv_kernel PAIR; causal only)
-static bool kv_pair() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ORION_ATTN_PAIR");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
 static bool delta_fused() {
   static int v = -1;
   if (v < 0) {
@@ -704,9 +682,7 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   const int pre_grid = (int)((rows * (D / 8) + 255) / 256);
   AttnParams q = p;
   q.delta = delta;
-  const int nkt = (p.Tk + 32 * 4 - 1) / (32 * 4);
-  const bool pair = causal && kv_pair();
-  const int kv_grid = (pair ? (nkt + 1) / 2 : nkt) * p.B * p.Hkv;
+  const int kv_grid = ((p.Tk + 32 * 4 - 1) / (32 * 4)) * p.B * p.Hkv;
   const int dq_grid = ((p.T + 127) / 128) * p.B * p.Hq;
   const bool fused = delta_fused();
   static const bool diag = getenv("ORION_ATTN_DIAG") && getenv("ORION_ATTN_DIAG")[0] == '1';
@@ -726,24 +702,21 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   if (p.bias_part) {  // packed self-attention with the QKV bias gradient (GPT-2: D = 64, MHA)
     if (D != 64 || fused || p.T != p.Tk || p.Hq != p.Hkv || p.T % 32) return -3;
 #define SPLITB(CC)                                                                                  \
-  split_attrs<64, CC>();                                                                            \
-  bias_attrs<CC>();                                                                                 \
   attn_delta_kernel<64, true><<<pre_grid, 256, 0, st>>>(q, delta);                                  \
-  kv_launch<64, CC>(q, kv_grid, pair, st);                                                          \
-  attn_bwd_dq_kernel<64, CC, false, true><<<dq_grid, 256, dq_lds(64), st>>>(q);
+  kv_launch<64, CC>(q, kv_grid, st);                                                                \
+  dq_launch<64, CC, false, true>(q, dq_grid, st);
     if (causal) { SPLITB(true) } else { SPLITB(false) }
 #undef SPLITB
     return (int)hipGetLastError();
   }
 #define SPLIT(DD, CC)                                                                   \
-  split_attrs<DD, CC>();                                                                \
   if (fused) {                                                                          \
-    attn_bwd_dq_kernel<DD, CC, true><<<dq_grid, 256, dq_lds(DD), st>>>(q);              \
-    kv_launch<DD, CC>(q, kv_grid, pair, st);                                            \
+    dq_launch<DD, CC, true>(q, dq_grid, st);                                            \
+    kv_launch<DD, CC>(q, kv_grid, st);                                                  \
   } else {                                                                              \
     attn_delta_kernel<DD><<<pre_grid, 256, 0, st>>>(p, delta);                          \
-    kv_launch<DD, CC>(q, kv_grid, pair, st);                                            \
-    attn_bwd_dq_kernel<DD, CC, false><<<dq_grid, 256, dq_lds(DD), st>>>(q);             \
+    kv_launch<DD, CC>(q, kv_grid, st);                                                  \
+    dq_launch<DD, CC, false>(q, dq_grid, st);                                           \
   }
   if (D == 64) {
     if (causal) { SPLIT(64, true) } else { SPLIT(64, false) }

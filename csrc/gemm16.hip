@@ -559,14 +559,6 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   issue_x(1);
   advance_x();
   wait_vm_exact<6>();
-  if ((g.flags & 128) && nitems > 1 && (lcl & 1)) {
-    // stagger (flags & 128): every other workgroup of an XCD starts half an item late, so
-    // the chip's epilogue store bursts alternate between two halves of the CUs instead of
-    // all 256 storing at once (the epilogue is store-bandwidth-bound when they do)
-    const unsigned long t0 = __builtin_amdgcn_s_memtime();
-    const unsigned long delay = (unsigned long)nkx * 1400;  // ~half of a k-tile's 2,800 cycles
-    while (__builtin_amdgcn_s_memtime() - t0 < delay) __builtin_amdgcn_s_sleep(8);
-  }
   if constexpr (STAMPS) stp[1] = __builtin_amdgcn_s_memtime();
   g_barrier();
   if (grp == 1) g_barrier();  // the stagger: group 1 runs one slot behind (kept across items)

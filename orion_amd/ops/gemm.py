@@ -94,8 +94,11 @@ def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
 
 
 def _hip_wins(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
-    # short-K forwards (GPT-2 qkv / attn-proj) in-tree with the packed bias epilogue measured
-    # 0.7-0.9 % slower end to end (profiles/ab/ab_fwd_shortk_r03o.log): forwards stay on hipBLASLt
+    # Plain forwards stay on hipBLASLt.  The short-K ones (GPT-2 qkv + bias, attn-proj) are
+    # faster in-tree in isolation since the persistent walk (988 / 912 vs 934 / 898 TF/s,
+    # profiles/ab/gemm16_persistent_stagger_peritem_r04.log) but still slower in the step:
+    # 1,085-1,088k vs 1,095-1,098k tok/s, 3 of 3 alternating pairs
+    # (profiles/ab/ab_shortk_fwd_r04.log; round 3: -0.7-0.9 %, ab_fwd_shortk_r03o.log).
     return w_kmajor
 
 

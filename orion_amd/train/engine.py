@@ -62,8 +62,9 @@ class Trainer:
     what bounds small models and small micro-batches."""
 
     GRAPH_WARMUP = 2
-    # The warm-up and the capture run every linear-layer GEMM on csrc/gemm.hip
-    # (ops.gemm.hip_gemms): in round 1 the captured hipBLASLt GEMMs faulted (memory-aperture
+    # The warm-up and the capture run every linear-layer GEMM on the in-tree gemm16 kernel
+    # (ops.gemm.hip_gemms; csrc/gemm.hip dispatches to csrc/gemm16.hip, the same kernel the
+    # eager step uses for dgrad / wgrad): in round 1 the captured hipBLASLt GEMMs faulted (memory-aperture
     # violation) on the third replay at 65,536 tokens per micro-batch and rocBLAS gave NaNs,
     # which is why capture used to be capped at 8,192 tokens.  With the in-tree GEMM every
     # kernel of the step takes its arguments by value, so a replay depends on no host-side

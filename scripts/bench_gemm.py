@@ -40,8 +40,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--check", action="store_true", help="compare outputs against torch")
     ap.add_argument("--cfgs", default="p", help="comma list of in-tree variants to time: p = gemm16's "
-                    "persistent walk (default), s = one workgroup per work item (gemm_diag(64)), "
-                    "t = persistent with the half-item stagger of odd workgroups (gemm_diag(128))")
+                    "persistent walk (default), s = one workgroup per work item (gemm_diag(64))")
     ap.add_argument("--square", type=int, default=0, help="also time an NT GEMM of this cube size")
     ap.add_argument("--only", default="", help="comma list of shape names to run")
     ap.add_argument("--llama", action="store_true", help="Llama-2-7B shapes (M = 16,384 tokens) instead")
@@ -104,7 +103,7 @@ def main():
                 blas = lambda: x @ w
         def with_cfg(c, f):
             def run():
-                ops.gemm_diag({"s": 64, "t": 128}.get(c, 0))
+                ops.gemm_diag({"s": 64}.get(c, 0))
                 return f()
             return run
         fns = {f"hip{c}": with_cfg(c, hip) for c in cfgs}

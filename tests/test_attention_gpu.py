@@ -169,6 +169,36 @@ def test_forward_deferred_rescale_growing_scores(D, causal):
     within_bf16_budget("o", o, want, base)
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("case", ["overflow", "underflow", "some_rows"])
+def test_attention_extreme_scores(D, causal, case):
+    """Score ranges that overflow / underflow exp2 against a fixed reference: overflow: scores
+    up to ~+400 (log2 units); underflow: every score shifted by ~-140 / -195 (a shift common
+    to a query's keys: the softmax is unchanged); some_rows: only a few query rows extreme.
+    Forward and backward (which reads the lse) against the fp32 reference, budgeted by SDPA
+    in bf16.  (Round 4 measured a forward without the running max -- exp2 against 0, the
+    reference path only for out-of-range blocks -- against these; it was no faster and was
+    not kept: docs/PERFORMANCE.md.)"""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    B, T, H = 1, 512, 2
+    q = torch.randn(B, T, H, D, device=DEV, generator=g)
+    k = torch.randn(B, T, H, D, device=DEV, generator=g)
+    v = torch.randn(B, T, H, D, device=DEV, generator=g)
+    do = torch.randn(B, T, H, D, device=DEV, generator=g)
+    if case == "overflow":
+        q = q * 6.0
+        k = k * 6.0
+    elif case == "underflow":
+        # q . k gains -(16 * 0.75 * D) on every key: -768 / -1536 raw, ~-140 / -195 log2 units
+        q[..., 0] = 16.0
+        k[..., 0] = -0.75 * D
+    else:
+        q[:, ::37] *= 12.0
+    q, k, v, do = (t.to(torch.bfloat16) for t in (q, k, v, do))
+    _check(_run(q, k, v, do, causal, SPLIT), _ref(q, k, v, do, causal), _sdpa_bf16(q, k, v, do, causal))
+
+
 @pytest.mark.parametrize("env", [{"ORION_ATTN_FWD": "v2"}])
 def test_forward_kernel_variants_match_reference(env):
     """The fallback forward kernel (attention.hip's 64-bit-addressed one, taken when offsets
