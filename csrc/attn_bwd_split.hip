@@ -387,6 +387,14 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_bwd_kv_kernel(A
     stamp(4);
   }
   if constexpr (STAMPS) {
+    // keep the computation alive (the stamped kernel stores no dK / dV; without this the
+    // compiler drops every MFMA and LDS read -- round 3's stamps timed that gutted kernel)
+    float chk = 0.f;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) chk += dka[db][r] + dva[db][r];
+    if (chk == 1.2345e-30f) p.dk[tid] = 0;
     if (lane == 0) {
       unsigned long long* out = reinterpret_cast<unsigned long long*>(p.dq) + ((long)blockIdx.x * NW + wv) * 8;
       for (int k = 0; k < 5; ++k) out[k] = st_acc[k];

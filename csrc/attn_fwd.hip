@@ -56,7 +56,11 @@ ORION_DEVICE bf16x8 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-template <int D, bool CAUSAL, int QB>
+// STAMPS (diagnostic instantiation, ORION_ATTN_FWD_DIAG=1, D = 64 causal): every wave sums
+// s_memtime deltas of the five phases of a key tile (stage write + next load issue, K reads +
+// S MFMA issue, softmax incl. the wait for S, V reads + PV issue, barrier) and writes them with
+// its active-tile count, tile count and lifetime over p.o (scripts/attn_fwd_stamps.py).
+template <int D, bool CAUSAL, int QB, bool STAMPS = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
   // QB query blocks of 32 rows per wave (D = 64: 2, one 64-key tile's K / V fragments feed
   // both blocks' MFMAs and the two softmax chains interleave with each other's MFMAs)
@@ -145,10 +149,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
     lsum[qb] = 0.f;
   }
 
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_prev = 0, st_begin = 0;
+  int st_n = 0;
+  auto stamp = [&](int k) {
+    if constexpr (STAMPS) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (k >= 0) st_acc[k] += t - st_prev;
+      st_prev = t;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   auto tile = [&](auto bufc, int t) {
     constexpr int buf = decltype(bufc)::value;
+    stamp(-1);
     if (t + 1 < ntiles) swrite(std::integral_constant<int, buf ^ 1>{});
     if (t + 2 < ntiles) gload(t + 2);
+    stamp(0);
     const int k0 = t * BN;
     const bf16_t* Ks = smem + buf * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
@@ -176,6 +193,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
         __builtin_amdgcn_sched_group_barrier(0x100, KBR * (D / 16), 0);
         __builtin_amdgcn_sched_group_barrier(0x008, QB * KBR * (D / 16), 0);
       }
+      stamp(1);
+      ++st_n;
       bf16x8 pf[QB][4];
       float alpha[QB];
 #pragma unroll
@@ -241,6 +260,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
             }
         lsum[qb] = fmaf(lsum[qb], alpha[qb], addf(addf(ps4[0], ps4[1]), addf(ps4[2], ps4[3])));
       }
+      stamp(2);
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
         bf16x8 vfr[4];
@@ -251,8 +271,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) oacc[qb][db] = mfma32(vfr[kk], pf[qb][kk], oacc[qb][db]);
       }
+      stamp(3);
     }
+    stamp(-1);
     __syncthreads();
+    stamp(4);
   };
 
   gload(0);
@@ -262,9 +285,33 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   if (ntiles > 1) gload(1);
   __syncthreads();
+  stamp(-1);
+  st_begin = st_prev;
   for (int t = 0; t < ntiles; t += 2) {
     tile(std::integral_constant<int, 0>{}, t);
     if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
+  }
+  if constexpr (STAMPS) {
+    // keep the whole computation alive (the stamped kernel stores no O): a checksum of the
+    // accumulators decides a store that never happens
+    float chk = 0.f;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      chk += lsum[qb] + m[qb];
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) chk += oacc[qb][db][r];
+    }
+    if (chk == 1.2345e-30f) p.lse[tid] = chk;
+    if (lane == 0) {
+      unsigned long long* out = reinterpret_cast<unsigned long long*>(p.o) + ((long)blockIdx.x * 4 + wv) * 8;
+      for (int k = 0; k < 5; ++k) out[k] = st_acc[k];
+      out[5] = (unsigned long long)st_n;
+      out[6] = (unsigned long long)ntiles;
+      out[7] = st_prev - st_begin;
+    }
+    return;
   }
 
 #pragma unroll
@@ -306,6 +353,15 @@ static void fwd3_attr() {
 
 template <int D, bool CAUSAL>
 static void fwd3_launch(const AttnParams& p, int qb64, size_t lds, hipStream_t st) {
+  if constexpr (D == 64 && CAUSAL) {
+    static const bool diag = getenv("ORION_ATTN_FWD_DIAG") && getenv("ORION_ATTN_FWD_DIAG")[0] == '1';
+    if (diag) {  // stamped instantiation: phase sums over p.o (scripts/attn_fwd_stamps.py)
+      (void)hipFuncSetAttribute((const void*)attn_fwd3_kernel<64, true, 2, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 64 * D * 2);
+      attn_fwd3_kernel<64, true, 2, true><<<((p.T + 255) / 256) * p.B * p.Hq, 256, lds, st>>>(p);
+      return;
+    }
+  }
   if constexpr (D == 64) {
     if (qb64 == 2) {
       fwd3_attr<D, CAUSAL, 2>();
