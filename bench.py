@@ -80,6 +80,11 @@ def parse():
     return ap.parse_args()
 
 
+def _per_item_walk() -> bool:
+    from orion_amd.ops.gemm import per_item_walk
+    return per_item_walk()
+
+
 def main():
     args = parse()
     from orion_amd.parallel import launch
@@ -256,6 +261,8 @@ def main():
             "dist_backend": args.dist_backend if world > 1 or args.zero1 == "on" else None,
             "zero1": bool(args.impl == "native" and trainer.zero1),
             "zero1_mode": args.zero1,
+            "gemm16_walk": ("per_item" if args.impl == "native" and dev.type == "cuda" and _per_item_walk()
+                            else "persistent"),
             "optimizer_state_gb_per_rank": (round(3 * 4 * trainer.opt.master.numel() / 2**30, 2)
                                             if args.impl == "native" else None),
             "allreduce_busbw_gbps": busbw,

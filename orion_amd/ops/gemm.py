@@ -93,6 +93,28 @@ def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
             and gemm16_addressable(ldx, K, N, w_kmajor))
 
 
+# gemm16's work walk.  Persistent (default): one workgroup per CU for the whole GEMM, all
+# 160 KB of LDS held.  A kernel that needs LDS -- RCCL's collectives do -- gets a CU only when a
+# gemm16 workgroup exits, i.e. at the end of the GEMM; one workgroup per work item frees each CU
+# every item (~20-40 us).  Under data parallelism the bucketed all-reduces / reduce-scatters
+# run beside the backward GEMMs, so the trainer switches to per-item walks when it has a
+# reducer over more than one rank (ORION_GEMM_DDP_PERSISTENT=1 keeps the persistent walk);
+# the per-item walk costs 1-6 % on the isolated GPT-2 shapes
+# (profiles/ab/gemm16_persistent_stagger_peritem_r04.log, column cfgs_TFs).
+_PER_ITEM = False
+
+
+def set_per_item_walk(on: bool) -> None:
+    """Select gemm16's one-workgroup-per-item walk (True) or the persistent walk (False)."""
+    global _PER_ITEM
+    _PER_ITEM = bool(on)
+    C().gemm_diag(64 if _PER_ITEM else 0)
+
+
+def per_item_walk() -> bool:
+    return _PER_ITEM
+
+
 def _hip_wins(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
     # Plain forwards stay on hipBLASLt.  The short-K ones (GPT-2 qkv + bias, attn-proj) are
     # faster in-tree in isolation since the persistent walk (988 / 912 vs 934 / 898 TF/s,
