@@ -126,6 +126,44 @@ ORION_DEVICE void wave_colsum_store(const f32x16 (&x)[NDB], float sc, bool valid
   }
 }
 
+// Store one lane's row of a dK / dQ accumulator set (lane = token, registers = d: d = 32 db +
+// (r & 3) + 8 (r >> 2) + 4 h32) as bf16, times `sc`; with rope tables, the inverse rotation
+// (rotate-half pairs d, d + D/2 = accumulators db, db + NDB/2 at the same r): the gradient
+// w.r.t. the unrotated input, dx1 = c g1 + s g2, dx2 = c g2 - s g1.
+template <int NDB>
+ORION_DEVICE void store_row_grad(const f32x16 (&acc)[NDB], float sc, bf16_t* __restrict__ dst, int h32,
+                                 const float* __restrict__ rc, const float* __restrict__ rs) {
+  constexpr int D = 32 * NDB, H = NDB / 2;
+  if (rc) {
+#pragma unroll
+    for (int db = 0; db < H; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = db * 32 + 8 * g4 + 4 * h32;
+        const f32x4 c = *reinterpret_cast<const f32x4*>(rc + d), sn = *reinterpret_cast<const f32x4*>(rs + d);
+        bf16x4 lo, hi;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float g1 = acc[db][4 * g4 + j] * sc, g2 = acc[db + H][4 * g4 + j] * sc;
+          lo[j] = f2bf(c[j] * g1 + sn[j] * g2);
+          hi[j] = f2bf(c[j] * g2 - sn[j] * g1);
+        }
+        *reinterpret_cast<bf16x4*>(dst + d) = lo;
+        *reinterpret_cast<bf16x4*>(dst + d + D / 2) = hi;
+      }
+    return;
+  }
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      bf16x4 v4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v4[j] = f2bf(acc[db][4 * g4 + j] * sc);
+      *reinterpret_cast<bf16x4*>(dst + db * 32 + 8 * g4 + 4 * h32) = v4;
+    }
+}
+
 // ============================================================================ dK / dV
 // NW waves x 32 keys per workgroup; query tiles of 32 rows double-buffered in LDS
 // (register staged: the next tile's loads are issued before this tile's MFMAs and written
@@ -140,12 +178,9 @@ __host__ __device__ constexpr int kv_waves() { return 4; }
 // s_memtime deltas of the five phases of a query tile (S/dP chain issue, softmax, dV/dK
 // issue, LDS stage write, barrier) and writes them with its active-tile count and lifetime
 // over p.dq (the dQ kernel is then skipped): scripts/attn_stamps.py, profiles/attn_r03/.
-// NW: waves (32 keys each) per workgroup.  8 (256 keys, one workgroup of two waves per SIMD
-// per CU) halves the Q / dO bytes streamed from L2 per MFMA against 4 (128 keys, two or
-// three 4-wave workgroups per CU).
-template <int D, bool CAUSAL, bool STAMPS = false, int NW = kv_waves<D>()>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_bwd_kv_kernel(AttnParams p) {
-  constexpr int NT = NW * 64;
+template <int D, bool CAUSAL, bool STAMPS = false>
+__global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
+  constexpr int NW = kv_waves<D>(), NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
   constexpr int QT = BMQ * D;            // Q / dO tile elements
   constexpr int NQC = BMQ * NCH;         // 16-byte chunks per Q (or dO) tile
@@ -409,19 +444,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_bwd_kv_kernel(A
   if (mykey < p.Tk) {
     bf16_t* dKb = p.dk + b * p.dk_sb + hk * p.dk_sh + (long)mykey * p.dk_st;
     bf16_t* dVb = p.dv + b * p.dv_sb + hk * p.dv_sh + (long)mykey * p.dv_st;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        bf16x4 k4, v4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          k4[j] = f2bf(dka[db][4 * g4 + j] * p.scale);
-          v4[j] = f2bf(dva[db][4 * g4 + j]);
-        }
-        *reinterpret_cast<bf16x4*>(dKb + db * 32 + 8 * g4 + 4 * h32) = k4;
-        *reinterpret_cast<bf16x4*>(dVb + db * 32 + 8 * g4 + 4 * h32) = v4;
-      }
+    const long rrow = (long)(mykey + p.rope_pos0) * (D / 2);
+    store_row_grad<NDB>(dka, p.scale, dKb, h32, p.rope_cos ? p.rope_cos + rrow : nullptr,
+                        p.rope_sin ? p.rope_sin + rrow : nullptr);
+    store_row_grad<NDB>(dva, 1.f, dVb, h32, nullptr, nullptr);
   }
 }
 
@@ -596,15 +622,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   if (myq < p.T) {
     ORION_DASSERT(b < p.B && hq < p.Hq);
     bf16_t* Qo = p.dq + b * p.dq_sb + hq * p.dq_sh + (long)myq * p.dq_st;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        bf16x4 v4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = f2bf(dq[db][4 * g4 + j] * p.scale);
-        *reinterpret_cast<bf16x4*>(Qo + db * 32 + 8 * g4 + 4 * h32) = v4;
-      }
+    const long rrow = (long)(myq + p.rope_pos0) * (D / 2);  // as the forward rope kernel (t + pos0)
+    store_row_grad<NDB>(dq, p.scale, Qo, h32, p.rope_cos ? p.rope_cos + rrow : nullptr,
+                        p.rope_sin ? p.rope_sin + rrow : nullptr);
   }
 }
 
@@ -619,35 +639,15 @@ static size_t kv_lds(int D) {
 }
 static size_t dq_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
 
-// ORION_ATTN_KV_NW=8: 8-wave (256-key) dK/dV workgroups at D = 64 (attn_bwd_kv_kernel NW)
-static int kv_nw() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ORION_ATTN_KV_NW");
-    v = (e && atoi(e) == 8) ? 8 : 4;
-  }
-  return v;
-}
-
-template <int D, bool CAUSAL, int NW>
-static void kv_launch_nw(const AttnParams& q, hipStream_t st) {
+template <int D, bool CAUSAL>
+static void kv_launch(const AttnParams& q, int grid, hipStream_t st) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, CAUSAL, false, NW>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, CAUSAL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(D));
     done = true;
   }
-  const int grid = ((q.Tk + 32 * NW - 1) / (32 * NW)) * q.B * q.Hkv;
-  attn_bwd_kv_kernel<D, CAUSAL, false, NW><<<grid, NW * 64, kv_lds(D), st>>>(q);
-}
-
-// D = 128 keeps 4 waves (its K fragments come from an LDS image sized for 128 keys)
-template <int D, bool CAUSAL>
-static void kv_launch(const AttnParams& q, int, hipStream_t st) {
-  if (D == 64 && kv_nw() == 8)
-    kv_launch_nw<D, CAUSAL, D == 64 ? 8 : 4>(q, st);
-  else
-    kv_launch_nw<D, CAUSAL, 4>(q, st);
+  attn_bwd_kv_kernel<D, CAUSAL><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
 }
 
 template <int D, bool CAUSAL, bool FUSE, bool BIAS = false>

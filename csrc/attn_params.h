@@ -34,6 +34,12 @@ struct AttnParams {
   // the QKV projection's bias gradient needs no pass over the packed dQKV
   float* bias_part;
   int bias_ld;
+  // split backward: the inverse rotary embedding of dQ / dK at their stores (the attention ran
+  // on rope(q), rope(k); the caller wants the gradient w.r.t. the unrotated projection).
+  // cos / sin tables [positions][D / 2] fp32, position of token t = t + rope_pos0; null: none.
+  const float* rope_cos;
+  const float* rope_sin;
+  int rope_pos0;
 };
 
 }  // namespace orion

@@ -805,7 +805,9 @@ bool attn_bwd_use_split(int D, int64_t flags) {
 // bf16 dQKV.
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
               const Tensor& o, const Tensor& lse, bool causal, double scale, Tensor dq, Tensor dk,
-              Tensor dv, int64_t flags, const c10::optional<Tensor>& bias_grad) {
+              Tensor dv, int64_t flags, const c10::optional<Tensor>& bias_grad,
+              const c10::optional<Tensor>& rope_cos, const c10::optional<Tensor>& rope_sin,
+              int64_t rope_pos0) {
   check_attn_inputs(q, k, v);
   check_bf16(dout, "dout");
   TORCH_CHECK(dout.stride(3) == 1 && o.stride(3) == 1, "dout/o head dim must be contiguous");
@@ -827,6 +829,30 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   p.dv = (unsigned short*)dv.data_ptr();
   p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
   p.flags = (int)flags;
+  // rope_cos / rope_sin: dq and dk come out w.r.t. the UNROTATED q / k (the inverse rotation at
+  // the split kernels' stores; the other forms run the rope kernel on them afterwards)
+  const bool want_rope = rope_cos.has_value() && rope_cos->defined();
+  if (want_rope) {
+    TORCH_CHECK(rope_sin.has_value() && rope_sin->defined(), "rope_sin missing");
+    for (const Tensor* t : {&*rope_cos, &*rope_sin})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2 &&
+                      t->size(1) == D / 2 && t->size(0) >= rope_pos0 + std::max(p.T, p.Tk) && rope_pos0 >= 0,
+                  "rope tables must be contiguous fp32 [>= pos0 + T][D / 2]");
+    TORCH_CHECK(!has_out(bias_grad, (long)(p.Hq + 2 * p.Hkv) * D, "bias_grad"),
+                "rope and the fused QKV bias gradient are exclusive");
+    p.rope_cos = rope_cos->data_ptr<float>();
+    p.rope_sin = rope_sin->data_ptr<float>();
+    p.rope_pos0 = (int)rope_pos0;
+  }
+  auto unrope = [&]() {  // the forms without the fused inverse rotation
+    if (!want_rope) return;
+    for (Tensor* g : {&dq, &dk})
+      check_launch(orion_rope(g->data_ptr(), g->stride(0), g->stride(1), g->stride(2), g->data_ptr(),
+                              g->stride(0), g->stride(1), g->stride(2), p.rope_cos, p.rope_sin,
+                              (int)g->size(0), (int)g->size(1), (int)g->size(2), D, (int)rope_pos0, -1.f,
+                              cur_stream()),
+                   "rope (inverse)");
+  };
   const long ld = (long)(p.Hq + 2 * p.Hkv) * D;
   const bool want_bias = has_out(bias_grad, ld, "bias_grad");
   Tensor bpart;
@@ -867,6 +893,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
     }
     p.bias_part = nullptr;
   }
+  p.rope_cos = p.rope_sin = nullptr;
   auto dq_acc = at::empty({p.B, p.Hq, p.T, D}, fopts);
   p.dq_acc = dq_acc.data_ptr<float>();
   check_launch(orion_attn_bwd(p, D, causal, delta.data_ptr<float>(), cur_stream()), "attn_bwd");
@@ -874,6 +901,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
                                      dq.stride(1), dq.stride(2), p.B, p.Hq, p.T, D, cur_stream()),
                "attn_dq_convert");
   if (want_bias) attn_bias_colsum_packed(dq, *bias_grad, p.B * p.T, ld);
+  unrope();
 }
 
 }  // namespace
@@ -909,7 +937,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int pos0, float sign) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int pos0, float sign) -> ()");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int flags=0, Tensor(d!)? bias_grad=None) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, float scale, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, int flags=0, Tensor(d!)? bias_grad=None, Tensor? rope_cos=None, Tensor? rope_sin=None, int rope_pos0=0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {

@@ -100,11 +100,11 @@ class _RopeFlashPacked(torch.autograd.Function):
 
     Forward: ONE rope launch rotates the adjacent q|k head range into a contiguous
     (B, T, Hq + Hkv, D) buffer; the attention kernel reads q and k as strided views of it
-    and v straight from the projection.  Backward: the attention kernel writes dq, dk and
-    dv into the three head ranges of ONE packed gradient buffer, and one in-place rope
-    launch (inverse rotation) fixes up the dq|dk range -- no zero-fill, slice copies or
-    gradient adds around the kernels (the per-view autograd path cost ~0.8 ms per
-    Llama-7B layer at 16k tokens, more than the rope kernels themselves)."""
+    and v straight from the projection.  Backward: the attention kernels write dq, dk and
+    dv into the three head ranges of ONE packed gradient buffer, dq and dk already
+    un-rotated (the inverse rotation at the split kernels' stores, csrc/attn_bwd_split.hip
+    store_row_grad; the other backward forms run the rope kernel after) -- no zero-fill,
+    slice copies, gradient adds or rope pass around the kernels."""
 
     @staticmethod
     def forward(ctx, qkv, n_q, n_kv, cos, sin, pos0):
@@ -124,8 +124,7 @@ class _RopeFlashPacked(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         C().attn_bwd(do.contiguous(), qk[:, :, :n_q], qk[:, :, n_q:], qkv[:, :, n_q + n_kv:], o, lse,
                      True, scale, dqkv[:, :, :n_q], dqkv[:, :, n_q:n_q + n_kv], dqkv[:, :, n_q + n_kv:],
-                     _bwd_flags())
-        C().rope_(dqkv[:, :, :n_q + n_kv], cos, sin, pos0, -1.0)
+                     _bwd_flags(), None, cos, sin, pos0)
         return dqkv, None, None, None, None, None
 
 

@@ -199,6 +199,32 @@ def test_attention_extreme_scores(D, causal, case):
     _check(_run(q, k, v, do, causal, SPLIT), _ref(q, k, v, do, causal), _sdpa_bf16(q, k, v, do, causal))
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("form", [0, SPLIT, FUSED])
+def test_backward_inverse_rope_forms(D, form):
+    """attn_bwd with rope tables returns dq / dk w.r.t. the unrotated q / k: the split kernels
+    rotate at their stores, the fused form runs the rope kernel after.  Both equal the plain
+    backward followed by the separate inverse rope launch (to bf16 rounding of the stores)."""
+    C = _C()
+    B, T, H, pos0 = 2, 256, 4, 5
+    q, k, v, do = _inputs(B, T, T, H, H, D, seed=9)
+    cos, sin = ref.rope_tables(T + pos0, D, device=DEV)
+    scale = 1.0 / math.sqrt(D)
+    o, lse = C.attn_fwd(q, k, v, True, scale)
+    outs = []
+    for rope in (False, True):
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        if rope:
+            C.attn_bwd(do, q, k, v, o, lse, True, scale, dq, dk, dv, form, None, cos, sin, pos0)
+        else:
+            C.attn_bwd(do, q, k, v, o, lse, True, scale, dq, dk, dv, form)
+            C.rope_(dq, cos, sin, pos0, -1.0)
+            C.rope_(dk, cos, sin, pos0, -1.0)
+        outs.append((dq, dk, dv))
+    for a, b in zip(*outs):
+        assert rel_err(a, b) < 6e-3, rel_err(a, b)
+
+
 @pytest.mark.parametrize("env", [{"ORION_ATTN_FWD": "v2"}])
 def test_forward_kernel_variants_match_reference(env):
     """The fallback forward kernel (attention.hip's 64-bit-addressed one, taken when offsets

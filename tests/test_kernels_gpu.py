@@ -156,12 +156,13 @@ def _sdpa_bf16(q, k, v, causal):
     return o.transpose(1, 2)
 
 
-@pytest.mark.parametrize("hq,hkv,pos0", [(8, 8, 0), (8, 2, 16)])
-def test_rope_attention_packed(hq, hkv, pos0):
+@pytest.mark.parametrize("hq,hkv,pos0,D", [(8, 8, 0, 128), (8, 2, 16, 128), (4, 4, 3, 64)])
+def test_rope_attention_packed(hq, hkv, pos0, D):
     """Fused rope + attention on a packed (B, T, Hq + 2 Hkv, D) projection (Llama path):
-    one node, gradient written straight into the packed buffer with in-place inverse rope."""
+    one node, gradient written straight into the packed buffer, dq / dk un-rotated at the
+    split backward kernels' stores."""
     torch.manual_seed(0)
-    B, T, D = 2, 256, 128
+    B, T = 2, 256
     qkv = bf(B, T, hq + 2 * hkv, D).requires_grad_()
     cos, sin = ref.rope_tables(T + pos0, D, device=DEV)
     o = ops.rope_attention_packed(qkv, hq, hkv, cos, sin, pos0)
