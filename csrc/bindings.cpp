@@ -844,11 +844,13 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
     p.rope_sin = rope_sin->data_ptr<float>();
     p.rope_pos0 = (int)rope_pos0;
   }
+  const float* rcos = p.rope_cos;  // kept: p's copies are cleared for the forms below
+  const float* rsin = p.rope_sin;
   auto unrope = [&]() {  // the forms without the fused inverse rotation
     if (!want_rope) return;
     for (Tensor* g : {&dq, &dk})
       check_launch(orion_rope(g->data_ptr(), g->stride(0), g->stride(1), g->stride(2), g->data_ptr(),
-                              g->stride(0), g->stride(1), g->stride(2), p.rope_cos, p.rope_sin,
+                              g->stride(0), g->stride(1), g->stride(2), rcos, rsin,
                               (int)g->size(0), (int)g->size(1), (int)g->size(2), D, (int)rope_pos0, -1.f,
                               cur_stream()),
                    "rope (inverse)");

@@ -227,6 +227,7 @@ int orion_rope(const void* x, long xsb, long xst, long xsh, void* y, long ysb, l
                long ysh, const float* cosv, const float* sinv, int B, int T, int H, int D,
                int pos0, float sign, hipStream_t st) {
   if (D % 16) return -1;
+  if (!cosv || !sinv || !x || !y) return -3;
   const long n = (long)B * T * H * (D / 16);
   long g = (n + 255) / 256;
   if (g > 4096) g = 4096;
