@@ -11,7 +11,6 @@ import os
 import sys
 
 import torch
-import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from orion_amd.ops._ext import C, load_ext  # noqa: E402
