@@ -9,7 +9,9 @@ per work item that happens every item (~20 us); with the persistent walk only at
 the whole GEMM.  This measures it on one GPU: a chain of backward-shaped GEMMs on a normal
 stream, and, 1 ms into it, a memory-bound kernel (a 64 MB copy, about what one ring step of a
 large bucket moves) on a HIGH-priority stream; the copy's time from its stream reaching it to
-its end (events) against the same copy alone.  Prints one JSON line per GEMM mode.
+its end (events) against the same copy alone; then the same with a 64 MB sum (a reduction
+kernel with an LDS stage, like RCCL's collectives).  Prints one JSON line per probe and GEMM
+mode.
 
 usage: python scripts/coresidency.py [--reps 5]"""
 import argparse
@@ -38,17 +40,29 @@ hi = torch.cuda.Stream(priority=-1)      # the high-priority stream (RCCL's own 
 lo = torch.cuda.current_stream()
 
 
-def copy_alone():
+acc = torch.empty((), device="cuda", dtype=torch.float32)
+
+
+def probe(kind):
+    """the second-stream kernel: a 64 MB copy (no LDS) or a 64 MB sum (a reduction kernel
+    with an LDS stage, as RCCL's collectives have)"""
+    if kind == "copy":
+        dst.copy_(src)
+    else:
+        torch.sum(src, dtype=torch.float32, out=acc)
+
+
+def copy_alone(kind="copy"):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(hi):
         e0.record()
-        dst.copy_(src)
+        probe(kind)
         e1.record()
     e1.synchronize()
     return e0.elapsed_time(e1)
 
 
-def copy_beside_gemms():
+def copy_beside_gemms(kind="copy"):
     for _ in range(2):
         ops.gemm(dy, w, True, 0, None, None)
     torch.cuda.synchronize()
@@ -61,22 +75,23 @@ def copy_beside_gemms():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(hi):
         e0.record()
-        dst.copy_(src)
+        probe(kind)
         e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1), g0.elapsed_time(g1)
 
 
-for _ in range(3):
-    copy_alone()
-alone = sorted(copy_alone() for _ in range(10))[5]
-for mode, flags in (("persistent", 0), ("per_item", 64)):
-    ops.gemm_diag(flags)
-    res = [copy_beside_gemms() for _ in range(a.reps)]
-    ops.gemm_diag(0)
-    cp = sorted(r[0] for r in res)
-    gm = sorted(r[1] for r in res)
-    print(json.dumps({"gemm_mode": mode, "copy_alone_ms": round(alone, 4),
-                      "copy_beside_gemm_ms_median": round(cp[len(cp) // 2], 4),
-                      "copy_beside_gemm_ms_max": round(cp[-1], 4),
-                      "gemm_chain_ms_median": round(gm[len(gm) // 2], 3)}), flush=True)
+for kind in ("copy", "sum"):
+    for _ in range(3):
+        copy_alone(kind)
+    alone = sorted(copy_alone(kind) for _ in range(10))[5]
+    for mode, flags in (("persistent", 0), ("per_item", 64)):
+        ops.gemm_diag(flags)
+        res = [copy_beside_gemms(kind) for _ in range(a.reps)]
+        ops.gemm_diag(0)
+        cp = sorted(r[0] for r in res)
+        gm = sorted(r[1] for r in res)
+        print(json.dumps({"probe": kind, "gemm_mode": mode, "probe_alone_ms": round(alone, 4),
+                          "probe_beside_gemm_ms_median": round(cp[len(cp) // 2], 4),
+                          "probe_beside_gemm_ms_max": round(cp[-1], 4),
+                          "gemm_chain_ms_median": round(gm[len(gm) // 2], 3)}), flush=True)

@@ -257,3 +257,23 @@ def test_swiglu_mlp_matches_reference():
     within_bf16_budget("y", y, yr, yb)
     for n, t, f, b in zip(("dx", "dwgu", "dwdown"), ts, fs, bs):
         within_bf16_budget(n, t.grad, f.grad, b.grad)
+
+
+def test_per_item_walk_is_bitwise_identical():
+    """ops.gemm.set_per_item_walk (what the trainer selects under multi-rank data parallelism,
+    so RCCL's kernels get CUs between work items) changes only which workgroup runs an item:
+    input gradients, fused epilogues and split-K weight gradients are bitwise identical."""
+    from orion_amd.ops import gemm as G
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x, w = _rnd(g, 4096, 768), _rnd(g, 768, 3072)
+    dy, xa = _rnd(g, 8192, 768), _rnd(g, 8192, 2304)
+    outs = []
+    for per_item in (False, True):
+        G.set_per_item_walk(per_item)
+        try:
+            assert G.per_item_walk() is per_item
+            outs.append((_C().gemm(x, w, True, 0, None, None)[0], G.wgrad(dy, xa)))
+        finally:
+            G.set_per_item_walk(False)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
