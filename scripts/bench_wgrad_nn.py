@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Weight gradient dW = dY^T X at the Llama-7B shapes (16,384 tokens): the phased in-tree kernel
-(both operands k-major; round 2 measured it on the since-removed csrc/gemm_phased.hip) vs transposing dY once (HBM pass) and running the
-library GEMM in the dgrad (NN) layout with fp32 output.  One JSON line per shape."""
+"""Weight gradient dW = dY^T X at the Llama-7B shapes (16,384 tokens): the in-tree kernel (both
+operands k-major; round 2 measured the since-removed csrc/gemm_phased.hip, now gemm16) vs
+transposing dY once (HBM pass) and running the library GEMM in the dgrad (NN) layout with fp32
+output.  One JSON line per shape."""
 import json
 import os
 import sys
