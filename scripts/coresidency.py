@@ -49,7 +49,7 @@ def probe(kind):
     if kind == "copy":
         dst.copy_(src)
     else:
-        torch.sum(src, dtype=torch.float32, out=acc)
+        torch.sum(src, dim=0, dtype=torch.float32, out=acc)
 
 
 def copy_alone(kind="copy"):
