@@ -178,9 +178,7 @@ __host__ __device__ constexpr int kv_waves() { return 4; }
 // s_memtime deltas of the five phases of a query tile (S/dP chain issue, softmax, dV/dK
 // issue, LDS stage write, barrier) and writes them with its active-tile count and lifetime
 // over p.dq (the dQ kernel is then skipped): scripts/attn_stamps.py, profiles/attn_r03/.
-// HF (A/B): every Q / dO fragment of a step read before the S / dP MFMAs (instead of each read
-// right before its MFMA, which the compiler issues into one register with a wait per MFMA).
-template <int D, bool CAUSAL, bool STAMPS = false, bool HF = false>
+template <int D, bool CAUSAL, bool STAMPS = false>
 __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(AttnParams p) {
   constexpr int NW = kv_waves<D>(), NT = NW * 64;
   constexpr int BNK = 32 * NW, BMQ = 32, NCH = D / 8, NDB = D / 32;
@@ -370,32 +368,15 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 #pragma unroll
         for (int j = 0; j < 4; ++j) { s[4 * g4 + j] = L[j]; dp[4 * g4 + j] = Dl[j]; }
       }
-      if constexpr (HF && !KLDS) {
-        bf16x8 qa[D / 16], da[D / 16];
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          const int o = loff<D>(l32, ks * 16 + 8 * h32);
-          qa[ks] = lds_b128(Qc, o);
-          da[ks] = lds_b128(Dc, o);
-        }
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          s = mfma32(qa[ks], kf[ks], s);
-          dp = mfma32(da[ks], vf[ks], dp);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * (D / 16) + 8, 0);  // every LDS read first
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * (D / 16), 0);
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          const int o = loff<D>(l32, ks * 16 + 8 * h32);
-          bf16x8 kfr;
-          if constexpr (KLDS) kfr = lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
-          else kfr = kf[ks];
-          s = mfma32(lds_b128(Qc, o), kfr, s);
-          dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
-          if constexpr (KLDS) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
-        }
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const int o = loff<D>(l32, ks * 16 + 8 * h32);
+        bf16x8 kfr;
+        if constexpr (KLDS) kfr = lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
+        else kfr = kf[ks];
+        s = mfma32(lds_b128(Qc, o), kfr, s);
+        dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
+        if constexpr (KLDS) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
       }
       stamp(0);
       ++st_n;
@@ -658,31 +639,15 @@ static size_t kv_lds(int D) {
 }
 static size_t dq_lds(int D) { return (size_t)2 * 2 * 64 * D * 2; }
 
-// ORION_ATTN_KV_HOIST=1: attn_bwd_kv_kernel HF at D = 64 (A/B)
-static bool kv_hoist() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ORION_ATTN_KV_HOIST");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-
-template <int D, bool CAUSAL, bool HF>
-static void kv_launch_hf(const AttnParams& q, int grid, hipStream_t st) {
+template <int D, bool CAUSAL>
+static void kv_launch(const AttnParams& q, int grid, hipStream_t st) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, CAUSAL, false, HF>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kv_kernel<D, CAUSAL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kv_lds(D));
     done = true;
   }
-  attn_bwd_kv_kernel<D, CAUSAL, false, HF><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
-}
-
-template <int D, bool CAUSAL>
-static void kv_launch(const AttnParams& q, int grid, hipStream_t st) {
-  if (D == 64 && kv_hoist()) kv_launch_hf<D, CAUSAL, D == 64>(q, grid, st);
-  else kv_launch_hf<D, CAUSAL, false>(q, grid, st);
+  attn_bwd_kv_kernel<D, CAUSAL><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
 }
 
 template <int D, bool CAUSAL, bool FUSE, bool BIAS = false>
