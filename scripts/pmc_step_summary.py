@@ -30,6 +30,8 @@ def group(name):
         return "GEMM gemm16 dgrad + GELU' + bias-grad epilogue"
     if "gemm16_kernel<false, false, 2" in n:
         return "GEMM gemm16 fwd + bias + GELU epilogue"
+    if "gemm16_kernel<false, true, 5" in n:
+        return "GEMM gemm16 dgrad + SwiGLU' epilogue"
     if "gemm16_kernel" in n:
         return "GEMM gemm16 input gradients"
     if "cijk" in n or "gemm[" in n:
