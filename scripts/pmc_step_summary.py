@@ -72,10 +72,13 @@ def main():
     d = sys.argv[1]
     m, f, w = load(d, "m"), load(d, "f"), load(d, "w")
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    other = collections.defaultdict(float)
     mk, fk, wk = list(m.values()), list(f.values()), list(w.values())
     for i, (name, c, ns) in enumerate(mk):
         g = agg[group(name)]
         g["n"] += 1
+        if group(name) == "other":
+            other[name[:70]] += ns
         g["ns"] += ns
         g["mfma"] += c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
         g["active"] += c.get("GRBM_GUI_ACTIVE", 0.0)
@@ -91,6 +94,9 @@ def main():
         gb = (g["fetch"] + g["write"]) / 1e9
         tbs = gb / (g["ns"] / 1e9) / 1e3 if g["ns"] else 0.0
         print(f"{k:44s} {g['ns'] / 1e6:8.2f} {100 * g['ns'] / tot:5.1f} {100 * util:8.1f}% {gb:8.2f} {tbs:6.2f}")
+    print("largest kernels in 'other' (ms):")
+    for k, ns in sorted(other.items(), key=lambda x: -x[1])[:8]:
+        print(f"  {k:70s} {ns / 1e6:8.2f}")
 
 
 if __name__ == "__main__":
