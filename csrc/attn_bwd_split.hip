@@ -368,6 +368,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 #pragma unroll
         for (int j = 0; j < 4; ++j) { s[4 * g4 + j] = L[j]; dp[4 * g4 + j] = Dl[j]; }
       }
+      mfma_prio(true);
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
         const int o = loff<D>(l32, ks * 16 + 8 * h32);
@@ -378,6 +379,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
         dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
         if constexpr (KLDS) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
       }
+      mfma_prio(false);
       stamp(0);
       ++st_n;
       // P and dS in place: row q = qbase + (r&3)+8(r>>2)+4*h32, column = mykey
@@ -406,6 +408,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
       sb[0] = acc_to_frag(dp, 0);
       sb[1] = acc_to_frag(dp, 1);
       stamp(1);
+      mfma_prio(true);
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
 #pragma unroll
@@ -414,6 +417,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
           dka[db] = mfma32(tr_frag<D>(Qc, 16 * s2 + 4 * h32, db * 32, lane, 8), sb[s2], dka[db]);
         }
       }
+      mfma_prio(false);
       stamp(2);
     }
     if (it + 1 < total) swrite(buf ^ 1);
@@ -572,12 +576,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
       const int k0 = t * BN + kb * 32;
       if (CAUSAL && k0 > qw0 + 31 + off) continue;  // wave-uniform: block fully masked
       f32x16 s = zero16(), dp = zero16();
+      mfma_prio(true);
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
         s = mfma32(lds_b128(Ks + kb * 32 * D, ko[ks]), qf[ks], s);
         dp = mfma32(lds_b128(Vs + kb * 32 * D, ko[ks]), df[ks], dp);
         if constexpr (D == 128) { if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0); }
       }
+      mfma_prio(false);
       // S^T / dP^T: row = key k0 + (r&3)+8(r>>2)+4*h32, column = this lane's query
       const bool need_mask = (CAUSAL && (k0 + 31 > qw0 + off)) || (k0 + 32 > p.Tk);
       if (need_mask) {
@@ -594,11 +600,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
       const bf16x8 ds0 = acc_to_frag(dp, 0), ds1 = acc_to_frag(dp, 1);
       // dQ^T += K^T dS^T: A = K^T by transposed reads of the K image (key order permuted
       // within each 16-key step exactly as the accumulator-as-operand dS^T fragment)
+      mfma_prio(true);
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
         dq[db] = mfma32(tr_frag<D>(Ks, kb * 32 + 4 * h32, db * 32, lane, 8), ds0, dq[db]);
         dq[db] = mfma32(tr_frag<D>(Ks, kb * 32 + 16 + 4 * h32, db * 32, lane, 8), ds1, dq[db]);
       }
+      mfma_prio(false);
     }
     if (t + 1 < ntiles) swrite(std::integral_constant<int, buf ^ 1>{});
     __syncthreads();

@@ -175,6 +175,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
       // block (8 of 16) at a time at D = 128, where 64 fragment registers would spill
       constexpr int KBR = D == 64 ? 2 : 1;  // key blocks per read group
       f32x16 s[QB][2];
+      mfma_prio(true);
 #pragma unroll
       for (int kg = 0; kg < 2; kg += KBR) {
         bf16x8 kfr[KBR][D / 16];
@@ -193,6 +194,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
         __builtin_amdgcn_sched_group_barrier(0x100, KBR * (D / 16), 0);
         __builtin_amdgcn_sched_group_barrier(0x008, QB * KBR * (D / 16), 0);
       }
+      mfma_prio(false);
       stamp(1);
       ++st_n;
       bf16x8 pf[QB][4];
@@ -261,6 +263,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
         lsum[qb] = fmaf(lsum[qb], alpha[qb], addf(addf(ps4[0], ps4[1]), addf(ps4[2], ps4[3])));
       }
       stamp(2);
+      mfma_prio(true);
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
         bf16x8 vfr[4];
@@ -271,6 +274,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) oacc[qb][db] = mfma32(vfr[kk], pf[qb][kk], oacc[qb][db]);
       }
+      mfma_prio(false);
       stamp(3);
     }
     stamp(-1);
