@@ -82,7 +82,10 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
             os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_time)
         if stale:
             base = bind if src.endswith(".cpp") else kern
-            jobs_list.append(base + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj])
+            extra = FILE_FLAGS.get(os.path.basename(src), [])
+            if os.path.basename(src).startswith("attn_"):  # scheduler-option A/B builds
+                extra = extra + os.environ.get("ORION_AMD_ATTN_FLAGS", "").split()
+            jobs_list.append(base + extra + ["-c", src, "-o", obj])
     jobs = jobs or min(8, os.cpu_count() or 4)
     if jobs_list:
         with cf.ThreadPoolExecutor(jobs) as ex:
