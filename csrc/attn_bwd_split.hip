@@ -259,6 +259,14 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
   unsigned vdo[NQ];
 #pragma unroll
   for (int i = 0; i < NQ; ++i) vdo[i] = qrow(i) * dst_b + qch(i) * 16;
+  // chunk i > 0 sits RSTEP rows below chunk 0 (same column): its load offset differs by a
+  // wave-uniform amount (carried in the scalar offset) and, the swizzle repeating every 16
+  // rows, its LDS offset by a constant -- one offset register per tensor instead of NQ (at
+  // D = 128 the kernel is at 256 VGPRs and the extra offsets were spilled, their reload
+  // waiting vmcnt(0) in front of every step's Q / dO load issue)
+  constexpr int RSTEP = NT / NCH;
+  constexpr bool ONEOFF = NSTQ >= 2 && RSTEP % 16 == 0;
+  const unsigned qstep = (unsigned)RSTEP * p.q_st * 2, dstep = (unsigned)RSTEP * p.do_st * 2;
   auto gload = [&](int h, int qi) {
     const int hq = hk * rep + h;
     const int qbase = qi * BMQ;
@@ -268,8 +276,8 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
       if constexpr (NSTQ >= 2) {
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
-          qdst[i] = bwd_buf_load16(rq, vq[i], sq);
-          qdst[NQ + i] = bwd_buf_load16(rd, vdo[i], sd);
+          qdst[i] = bwd_buf_load16(rq, ONEOFF ? vq[0] : vq[i], ONEOFF ? sq + i * qstep : sq);
+          qdst[NQ + i] = bwd_buf_load16(rd, ONEOFF ? vdo[0] : vdo[i], ONEOFF ? sd + i * dstep : sd);
         }
       } else {
         qdst[0] = isd ? bwd_buf_load16(rd, vq[0], sd) : bwd_buf_load16(rq, vq[0], sq);
@@ -302,8 +310,9 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
     if constexpr (NSTQ >= 2) {
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
-        *reinterpret_cast<bf16x8*>(Qs + buf * QT + qlo_[i]) = qdst[i];
-        *reinterpret_cast<bf16x8*>(Ds + buf * QT + qlo_[i]) = qdst[NQ + i];
+        const int lo = ONEOFF ? qlo_[0] + i * RSTEP * D : qlo_[i];
+        *reinterpret_cast<bf16x8*>(Qs + buf * QT + lo) = qdst[i];
+        *reinterpret_cast<bf16x8*>(Ds + buf * QT + lo) = qdst[NQ + i];
       }
     } else {
       *reinterpret_cast<bf16x8*>((isd ? Ds : Qs) + buf * QT + qlo_[0]) = qdst[0];
@@ -368,12 +377,21 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 #pragma unroll
         for (int j = 0; j < 4; ++j) { s[4 * g4 + j] = L[j]; dp[4 * g4 + j] = Dl[j]; }
       }
+      // D = 128: the per-fragment LDS offsets are rebuilt each step from one opaque per-lane
+      // base (an xor and a shift per read) instead of being held as 16 loop-invariant
+      // registers -- at 256 VGPRs those pushed V fragments / offsets into scratch, and each
+      // reload waited vmcnt(0) behind the step's Q / dO prefetch.  Column chunk 2 ks + h32 of
+      // row l32 sits at chunk (2 ks) ^ (h32 ^ swz(l32)); rows wv * 32 + l32 of the K image
+      // share the swizzle of row l32 (period 16).
+      int zb = (l32 * D) | ((h32 ^ swz<D>(l32)) << 3);
+      if constexpr (KLDS) asm volatile("" : "+v"(zb));
+      const bf16_t* Kw = Ks + wv * 32 * D;
       mfma_prio(true);
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        const int o = loff<D>(l32, ks * 16 + 8 * h32);
+        const int o = KLDS ? (zb ^ (ks << 4)) : loff<D>(l32, ks * 16 + 8 * h32);
         bf16x8 kfr;
-        if constexpr (KLDS) kfr = lds_b128(Ks, loff<D>(wv * 32 + l32, ks * 16 + 8 * h32));
+        if constexpr (KLDS) kfr = lds_b128(Kw, o);
         else kfr = kf[ks];
         s = mfma32(lds_b128(Qc, o), kfr, s);
         dp = mfma32(lds_b128(Dc, o), vf[ks], dp);
