@@ -36,6 +36,7 @@ int orion_scale_bf16(void*, const float*, long, hipStream_t);
 int orion_slab_sum(const float*, int, long, void*, const float*, int, int, hipStream_t);
 int orion_wgrad_splits(int, int, int);
 int orion_wgrad_effective_splits(int, int);
+int orion_wgrad_tail_rows(int, int, int, int*);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
                 const float*, int, int, hipStream_t);
 int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
@@ -453,7 +454,21 @@ void wgrad_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& 
     TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "scale must be one fp32");
     sc = scale->data_ptr<float>();
   }
-  if (S > 1) {
+  int S2 = 1;
+  const int R1 = splits > 0 ? 0 : orion_wgrad_tail_rows(M, N1, N2, &S2);
+  if (R1 > 0) {  // whole rounds unsplit, the tail rows split-K (orion_wgrad_tail_rows)
+    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, R1, N2, 1,
+                             nullptr, out.data_ptr(), sc, accumulate ? 1 : 0, is_f32(out),
+                             cur_stream()), "wgrad head");
+    const int N1t = N1 - R1;
+    auto slabs = at::empty({S2, N1t, N2}, dy.options().dtype(at::kFloat));
+    const auto* dyt = static_cast<const char*>(dy.data_ptr()) + (size_t)R1 * dy.element_size();
+    auto* outt = static_cast<char*>(out.data_ptr()) + (size_t)R1 * N2 * out.element_size();
+    check_launch(orion_wgrad(dyt, dy.stride(0), x.data_ptr(), x.stride(0), M, N1t, N2, S2,
+                             slabs.data_ptr<float>(), nullptr, nullptr, 0, 0, cur_stream()), "wgrad tail");
+    check_launch(orion_slab_sum(slabs.data_ptr<float>(), S2, (long)N1t * N2, outt, sc,
+                                accumulate ? 1 : 0, is_f32(out), cur_stream()), "wgrad tail slab_sum");
+  } else if (S > 1) {
     auto slabs = at::empty({S, N1, N2}, dy.options().dtype(at::kFloat));
     check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, S,
                              slabs.data_ptr<float>(), nullptr, nullptr, 0, 0, cur_stream()), "wgrad");

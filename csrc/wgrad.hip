@@ -211,6 +211,28 @@ int orion_wgrad_splits(int M, int N1, int N2) {
   return bestS;
 }
 
+// Tail split of an unsplit weight gradient whose tile count leaves a partial last round
+// (one workgroup per CU, 256 CUs): the first R1 output rows form whole rounds and run
+// unsplit; the remaining rows -- at most half a round of tiles -- run split-K over S2 =
+// 256 / tail-tiles chunks, so the last round costs 1 / S2 of an item instead of a whole one.
+// Llama-7B gate_up (22,016 x 4,096: 1,376 tiles, 5.4 rounds): 80 rows of tiles unsplit +
+// 6 rows at S2 = 2 -- 5.5 instead of 6 item times.  Returns R1 (0: no split) and S2.
+int orion_wgrad_effective_splits(int M, int S);
+
+int orion_wgrad_tail_rows(int M, int N1, int N2, int* S2) {
+  *S2 = 1;
+  if (orion_wgrad_splits(M, N1, N2) != 1 || N1 % 256) return 0;
+  const long t1 = N1 / 256, t2 = (N2 + 255) / 256, tiles = t1 * t2;
+  const long rem = tiles % 256;
+  if (tiles <= 256 || rem == 0 || rem > 128) return 0;
+  const long head = tiles - rem;
+  if (head % t2) return 0;  // the whole rounds must be whole rows of tiles
+  const int s2 = orion_wgrad_effective_splits(M, (int)(256 / rem));
+  if (s2 < 2) return 0;
+  *S2 = s2;
+  return (int)(head / t2) * 256;
+}
+
 // number of k-chunks actually produced when S are requested (chunks are whole stages)
 int orion_wgrad_effective_splits(int M, int S) {
   if (S < 1) S = 1;

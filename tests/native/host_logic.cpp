@@ -12,6 +12,7 @@
 
 int orion_wgrad_splits(int M, int N1, int N2);
 int orion_wgrad_effective_splits(int M, int S);
+int orion_wgrad_tail_rows(int M, int N1, int N2, int* S2);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
                 const float*, int, int, hipStream_t);
 int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, void*, long,
@@ -46,6 +47,26 @@ int main() {
           CHECK(e >= 1 && e <= req);
         }
       }
+  // tail split: head rows are whole rounds of whole tile rows, the tail at most half a round
+  for (int M : Ms)
+    for (int n1 : Ns)
+      for (int n2 : Ns) {
+        int S2 = 0;
+        const int R1 = orion_wgrad_tail_rows(M, n1, n2, &S2);
+        CHECK(R1 >= 0 && R1 < n1 && R1 % 256 == 0);
+        if (R1 > 0) {
+          const long t2 = (n2 + 255) / 256, head = (long)(R1 / 256) * t2, tail = (long)(n1 - R1) / 256 * t2;
+          CHECK(head % 256 == 0 && tail > 0 && tail <= 128);
+          CHECK(S2 >= 2 && tail * S2 <= 256 && orion_wgrad_effective_splits(M, S2) == S2);
+        } else {
+          CHECK(S2 == 1);
+        }
+      }
+  {  // Llama-7B gate_up weight gradient at 16k tokens: 80 tile rows unsplit + 6 rows at S2 = 2
+    int S2 = 0;
+    CHECK(orion_wgrad_tail_rows(16384, 22016, 4096, &S2) == 80 * 256 && S2 == 2);
+    CHECK(orion_wgrad_tail_rows(16384, 12288, 4096, &S2) == 0);  // 768 tiles: whole rounds
+  }
   // scratch sizing is monotone and positive
   for (int rows = 1; rows < (1 << 20); rows = rows * 3 + 1) {
     CHECK(orion_layernorm_bwd_blocks(rows) >= 1 && orion_layernorm_bwd_blocks(rows) <= 1024);

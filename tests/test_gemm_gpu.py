@@ -181,12 +181,13 @@ def test_gemm_batched_input_shape_and_strided_rows():
 
 
 @pytest.mark.parametrize("M,N1,N2", [(8192, 264, 136), (65536, 768, 768), (4096, 3072, 768), (8224, 200, 264),
-                                     (16384, 50304, 768)])
+                                     (16384, 50304, 768), (2048, 22016, 4096)])
 @pytest.mark.parametrize("acc", [False, True])
 def test_wgrad_into_fp32(M, N1, N2, acc, gemm_cfg):
     """Weight gradients on gemm16 (split-K work items into fp32 slabs, or straight into the
     arena) into an fp32 arena slice, overwrite and accumulate; 8224 tokens (not a multiple of
-    64) take csrc/wgrad.hip's 32-row kernel; 50,304 x 768 is the LM head."""
+    64) take csrc/wgrad.hip's 32-row kernel; 50,304 x 768 is the LM head; 22,016 x 4,096 (Llama
+    gate_up) takes the tail split (80 tile rows unsplit, 6 rows split-K into slabs)."""
     g = torch.Generator(device=DEV).manual_seed(M + N1)
     dy, x = _rnd(g, M, N1), _rnd(g, M, N2)
     out = torch.randn(N1, N2, device=DEV, generator=g)
@@ -195,6 +196,20 @@ def test_wgrad_into_fp32(M, N1, N2, acc, gemm_cfg):
     want = dy.float().t() @ x.float() + (base if acc else 0)
     # fp32 output, fp32 accumulation: far below any bf16 budget
     assert rel_err(out, want) < 1e-4
+
+
+def test_wgrad_tail_split_bf16_scaled():
+    """The tail-split weight gradient into a bf16 output with a device scale: head rows and
+    tail rows both scaled once (the head in its epilogue, the tail in the slab sum)."""
+    g = torch.Generator(device=DEV).manual_seed(7)
+    M, N1, N2 = 2048, 22016, 4096
+    assert _C().wgrad_splits(M, N1, N2) == 1
+    dy, x = _rnd(g, M, N1), _rnd(g, M, N2)
+    sc = torch.tensor([0.25], device=DEV)
+    out = _C().wgrad(dy, x, sc, 0)
+    want = (dy.float().t() @ x.float()) * 0.25
+    within_bf16_budget("dw", out, want, ((dy.t() @ x).float() * 0.25).bfloat16())
+    assert rel_err(out[:20480], want[:20480]) < 5e-3 and rel_err(out[20480:], want[20480:]) < 5e-3
 
 
 @pytest.mark.parametrize("wkm", [False, True])
