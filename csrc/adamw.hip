@@ -8,28 +8,44 @@
 // 26 bytes/element of HBM traffic: the 124M-parameter step is ~3.2 GB, ~0.6 ms.
 #include "common.h"
 
+// non-temporal loads / stores for the once-per-step streams (A/B builds: -DADAMW_NT=0/1)
+#ifndef ADAMW_NT
+#define ADAMW_NT 1  // Llama-7B step: AdamW 33.6 vs 34.3 ms, grad norm 4.32 vs 4.44 (profiles/ab/adamw_nt_r04.log)
+#endif
+
 namespace orion {
+
+template <typename T>
+ORION_DEVICE T ld_stream(const T* p) {
+  if constexpr (ADAMW_NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T>
+ORION_DEVICE void st_stream(T v, T* p) {
+  if constexpr (ADAMW_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
 constexpr int ADAM_CHUNK = 2048;  // must match orion_amd/train/flat.py ALIGN
 
 // 8 consecutive gradient elements as fp32 (arena in fp32 or bf16)
 ORION_DEVICE void load8(const float* g, long e, float (&f)[8]) {
-  const f32x4 a = *reinterpret_cast<const f32x4*>(g + e), b = *reinterpret_cast<const f32x4*>(g + e + 4);
+  const f32x4 a = ld_stream(reinterpret_cast<const f32x4*>(g + e)), b = ld_stream(reinterpret_cast<const f32x4*>(g + e + 4));
 #pragma unroll
   for (int j = 0; j < 4; ++j) { f[j] = a[j]; f[4 + j] = b[j]; }
 }
 ORION_DEVICE void load8(const bf16_t* g, long e, float (&f)[8]) {
-  const bf16x8 v = *reinterpret_cast<const bf16x8*>(g + e);
+  const bf16x8 v = ld_stream(reinterpret_cast<const bf16x8*>(g + e));
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
 }
 ORION_DEVICE void load4(const float* g, long e, float (&f)[4]) {
-  const f32x4 a = *reinterpret_cast<const f32x4*>(g + e);
+  const f32x4 a = ld_stream(reinterpret_cast<const f32x4*>(g + e));
 #pragma unroll
   for (int j = 0; j < 4; ++j) f[j] = a[j];
 }
 ORION_DEVICE void load4(const bf16_t* g, long e, float (&f)[4]) {
-  const bf16x4 v = *reinterpret_cast<const bf16x4*>(g + e);
+  const bf16x4 v = ld_stream(reinterpret_cast<const bf16x4*>(g + e));
 #pragma unroll
   for (int j = 0; j < 4; ++j) f[j] = bf2f(v[j]);
 }
@@ -77,9 +93,9 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     const long e = i * 4;
     const float dec = decay[e / ADAM_CHUNK] ? (1.f - lr * wd) : 1.f;
-    f32x4 w = *reinterpret_cast<const f32x4*>(master + e);
-    f32x4 mm = *reinterpret_cast<const f32x4*>(m + e);
-    f32x4 vv = *reinterpret_cast<const f32x4*>(v + e);
+    f32x4 w = ld_stream(reinterpret_cast<const f32x4*>(master + e));
+    f32x4 mm = ld_stream(reinterpret_cast<const f32x4*>(m + e));
+    f32x4 vv = ld_stream(reinterpret_cast<const f32x4*>(v + e));
     float gg[4];
     load4(g, e, gg);
     bf16x4 out;
@@ -92,10 +108,10 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
       w[j] = w[j] * dec - step * mm[j] / denom;
       out[j] = f2bf(w[j]);
     }
-    *reinterpret_cast<f32x4*>(master + e) = w;
-    *reinterpret_cast<f32x4*>(m + e) = mm;
-    *reinterpret_cast<f32x4*>(v + e) = vv;
-    *reinterpret_cast<bf16x4*>(p16 + e) = out;
+    st_stream(w, reinterpret_cast<f32x4*>(master + e));
+    st_stream(mm, reinterpret_cast<f32x4*>(m + e));
+    st_stream(vv, reinterpret_cast<f32x4*>(v + e));
+    st_stream(out, reinterpret_cast<bf16x4*>(p16 + e));
   }
 }
 

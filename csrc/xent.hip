@@ -12,6 +12,14 @@
 #include "common.h"
 #include "mfma_lds.h"
 
+// cache-policy bits of the row's buffer loads / stores (A/B builds: -DXENT_LD_AUX=..)
+#ifndef XENT_LD_AUX
+#define XENT_LD_AUX 2  // nt: the row is streamed once (2.34 vs 2.66 ms per GPT-2 step, profiles/ab/xent_nt_r04.log)
+#endif
+#ifndef XENT_ST_AUX
+#define XENT_ST_AUX 2
+#endif
+
 namespace orion {
 
 
@@ -82,7 +90,7 @@ __global__ __launch_bounds__(XT, (XT == 512 ? 4 : 2)) void xent_fwd_bwd_kernel(
   for (int k = 0; k < CH; ++k) {
     const int c = k * XT + threadIdx.x;
     if (c < V8) {
-      v[k] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, vo, k * XT * 16, 0));
+      v[k] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, vo, k * XT * 16, XENT_LD_AUX));
       float a = fmaxf(fmaxf(bf2f(v[k][0]), bf2f(v[k][1])), bf2f(v[k][2]));
       a = fmaxf(fmaxf(a, bf2f(v[k][3])), bf2f(v[k][4]));
       a = fmaxf(fmaxf(a, bf2f(v[k][5])), bf2f(v[k][6]));
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(XT, (XT == 512 ? 4 : 2)) void xent_fwd_bwd_kernel(
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(v[k][j]) * f);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rr, vo, k * XT * 16, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rr, vo, k * XT * 16, XENT_ST_AUX);
     }
   }
   if (owner) {  // the target's own term (after this thread's store of its chunk)

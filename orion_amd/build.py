@@ -82,8 +82,12 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
             os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_time)
         if stale:
             base = bind if src.endswith(".cpp") else kern
-            extra = FILE_FLAGS.get(os.path.basename(src), [])
-            if os.path.basename(src).startswith("attn_"):  # scheduler-option A/B builds
+            name = os.path.basename(src)
+            extra = FILE_FLAGS.get(name, [])
+            # A/B builds: ORION_AMD_FLAGS_<STEM> (e.g. ORION_AMD_FLAGS_XENT) adds flags to one
+            # source; ORION_AMD_ATTN_FLAGS to both attention sources
+            extra = extra + os.environ.get("ORION_AMD_FLAGS_" + name.split(".")[0].upper(), "").split()
+            if name.startswith("attn_"):
                 extra = extra + os.environ.get("ORION_AMD_ATTN_FLAGS", "").split()
             jobs_list.append(base + extra + ["-c", src, "-o", obj])
     jobs = jobs or min(8, os.cpu_count() or 4)
