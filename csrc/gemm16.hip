@@ -84,6 +84,10 @@ ORION_DEVICE G16Item g16_decode(const GemmArgs& g, int w) {
 
 }  // namespace
 
+#ifndef G16_PRE_NT
+#define G16_PRE_NT 1  // GPT-2 step: the fc2 / attn-proj forwards that read the GELU output next 166 -> 156 us (profiles/ab/gemm16_pre_nt_r04.log)
+#endif
+
 // The epilogue of one work item (registers only, no LDS).
 template <int EPI>
 ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16Item& it, int wm, int grp,
@@ -229,7 +233,9 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       u32x4 pk;
 #pragma unroll
       for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(v[e]);
-      __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, 0);
+      // bias + GELU: the pre-activation is read again only by the backward -- streamed past
+      // the caches (G16_PRE_NT)
+      __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, (EPI == EPI_BIAS_GELU && G16_PRE_NT) ? 2 : 0);
       if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
         const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
 #pragma unroll

@@ -12,7 +12,31 @@
 //     sums, a second tiny kernel folds them (deterministic, no float atomics).
 #include "common.h"
 
+// LN_NT: the residual stream sum (saved for the backward, read again by the next block's norm
+// several kernels later) is stored, and the far operands (the incoming residual; the saved
+// input in the backward) are loaded, with the non-temporal hint, so the caches keep what the
+// NEXT kernel reads (the normalised output, the incoming gradient).
+#ifndef LN_NT
+#define LN_NT 1  // GPT-2 step: LayerNorm backward 78.5 vs 83.1 us, the GEMMs after it 1-2 % (profiles/ab/ln_nt_r04.log)
+#endif
+
 namespace orion {
+
+template <typename T>
+ORION_DEVICE T ld_far(const T* p) {
+  if constexpr (LN_NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <int VEC>
+ORION_DEVICE void store_vec_far(bf16_t* p, const float* in) {
+  typedef typename VecT<VEC>::type V;
+  V v;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) v[j] = f2bf(in[j]);
+  if constexpr (LN_NT) __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
+  else *reinterpret_cast<V*>(p) = v;
+}
 
 template <int VEC>
 ORION_DEVICE void load_vec(const bf16_t* p, float* out) {
@@ -69,7 +93,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   for (int i = 0; i < ITERS; ++i) {
     const int cl = min((i * 64 + lane) * VEC, C - VEC);
     xv[i] = *reinterpret_cast<const VT*>(xr + cl);
-    rvv[i] = *reinterpret_cast<const VT*>(rp + cl);
+    rvv[i] = ld_far(reinterpret_cast<const VT*>(rp + cl));
     rbv[i] = *reinterpret_cast<const VT*>(rbp + cl);
     wv[i] = *reinterpret_cast<const VT*>(w + cl);
     bvv[i] = *reinterpret_cast<const VT*>(bp + cl);
@@ -92,7 +116,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
         }
 #pragma unroll
         for (int j = 0; j < VEC; ++j) v[i][j] = bf2f(f2bf(v[i][j] + rv[j]));
-        store_vec<VEC>(sum_out + (size_t)row * C + c, v[i]);
+        store_vec_far<VEC>(sum_out + (size_t)row * C + c, v[i]);
       }
 #pragma unroll
       for (int j = 0; j < VEC; ++j) s += v[i][j];
@@ -170,7 +194,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int i = 0; i < ITERS; ++i) {
       const int c = (i * 64 + lane) * VEC;
       if (EXACT || c < C) {
-        xr[i] = *reinterpret_cast<const V*>(x + (size_t)rw * C + c);
+        xr[i] = ld_far(reinterpret_cast<const V*>(x + (size_t)rw * C + c));
         dyr[i] = *reinterpret_cast<const V*>(dy + (size_t)rw * C + c);
         if (dres) rr[i] = *reinterpret_cast<const V*>(dres + (size_t)rw * C + c);
       }
