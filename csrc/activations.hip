@@ -134,8 +134,21 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
                                                        int accumulate, int f32) {
   const float sc = scale ? *scale : 1.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    f32x4 acc = reinterpret_cast<const f32x4*>(slabs)[i];
-    for (int k = 1; k < S; ++k) acc += reinterpret_cast<const f32x4*>(slabs + (long)k * n4 * 4)[i];
+    // slabs in fixed order 0, 1, ..., S - 1 (deterministic), loaded 8 at a time (measured
+    // 14.1 vs 14.7 us per call: the sums are bound by the ~66 MB of slabs each reads,
+    // profiles/ab/slab_sum_unroll_r04.log)
+    const f32x4* sp = reinterpret_cast<const f32x4*>(slabs) + i;
+    const long sstride = n4;
+    f32x4 acc = sp[0];
+    for (int k = 1; k < S; k += 8) {  // S is uniform: the guards are scalar branches
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k + u < S) t[u] = sp[(k + u) * sstride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k + u < S) acc += t[u];
+    }
     acc *= sc;
     if (f32) {
       f32x4* o = reinterpret_cast<f32x4*>(out) + i;
