@@ -185,7 +185,12 @@ def pg_timeout() -> datetime.timedelta:
 def rccl_debug_env(log_dir: str, rank: int) -> str:
     """Route RCCL's INFO log (topology, rings/trees, channels) of this rank to a file before
     the communicator exists; returns the file's path.  Leaves a user's own NCCL_DEBUG alone."""
-    os.makedirs(log_dir, exist_ok=True)
+    try:
+        os.makedirs(log_dir, exist_ok=True)
+    except OSError:  # read-only tree: the log goes to the temp dir instead of failing the job
+        import tempfile
+        log_dir = os.path.join(tempfile.gettempdir(), "orion_rccl_logs")
+        os.makedirs(log_dir, exist_ok=True)
     path = os.path.join(log_dir, f"rccl_rank{rank}.log")
     if "NCCL_DEBUG" not in os.environ:
         os.environ["NCCL_DEBUG"] = "INFO"
