@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
         for (int j = 0; j < 4; ++j) { s[4 * g4 + j] = L[j]; dp[4 * g4 + j] = Dl[j]; }
       }
       // D = 128: the per-fragment LDS offsets are rebuilt each step from one opaque per-lane
-      // base (an xor and a shift per read) instead of being held as 16 loop-invariant
+      // base (one xor per read) instead of being held as 16 loop-invariant
       // registers -- at 256 VGPRs those pushed V fragments / offsets into scratch, and each
       // reload waited vmcnt(0) behind the step's Q / dO prefetch.  Column chunk 2 ks + h32 of
       // row l32 sits at chunk (2 ks) ^ (h32 ^ swz(l32)); rows wv * 32 + l32 of the K image
