@@ -34,6 +34,7 @@ g = torch.Generator(device="cuda").manual_seed(0)
 rnd = lambda *s: (torch.randn(*s, device="cuda", generator=g) * 0.5).to(torch.bfloat16)  # noqa: E731
 M = 65536
 dy, w = rnd(M, 768), rnd(768, 3072)       # fc input gradient shape (K = 768, N = 3072)
+xf, wf = rnd(M, 768), rnd(768, 3072)      # fc forward shape for the hipBLASLt chain
 src = torch.empty(32 * 1024 * 1024, device="cuda", dtype=torch.bfloat16)
 dst = torch.empty_like(src)
 hi = torch.cuda.Stream(priority=-1)      # the high-priority stream (RCCL's own stream is one)
@@ -62,14 +63,19 @@ def copy_alone(kind="copy"):
     return e0.elapsed_time(e1)
 
 
-def copy_beside_gemms(kind="copy"):
+def copy_beside_gemms(kind="copy", blas=False):
+    def one():
+        if blas:
+            torch.mm(xf, wf)
+        else:
+            ops.gemm(dy, w, True, 0, None, None)
     for _ in range(2):
-        ops.gemm(dy, w, True, 0, None, None)
+        one()
     torch.cuda.synchronize()
     g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     g0.record(lo)
     for _ in range(12):                   # ~5 ms of GEMMs
-        ops.gemm(dy, w, True, 0, None, None)
+        one()
     g1.record(lo)
     time.sleep(0.001)                     # the copy arrives mid-chain
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -85,9 +91,9 @@ for kind in ("copy", "sum"):
     for _ in range(3):
         copy_alone(kind)
     alone = sorted(copy_alone(kind) for _ in range(10))[5]
-    for mode, flags in (("persistent", 0), ("per_item", 64)):
+    for mode, flags in (("persistent", 0), ("per_item", 64), ("hipblaslt", 0)):
         ops.gemm_diag(flags)
-        res = [copy_beside_gemms(kind) for _ in range(a.reps)]
+        res = [copy_beside_gemms(kind, mode == "hipblaslt") for _ in range(a.reps)]
         ops.gemm_diag(0)
         cp = sorted(r[0] for r in res)
         gm = sorted(r[1] for r in res)
