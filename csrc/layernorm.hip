@@ -20,6 +20,10 @@
 #define LN_NT 1  // GPT-2 step: LayerNorm backward 78.5 vs 83.1 us, the GEMMs after it 1-2 % (profiles/ab/ln_nt_r04.log)
 #endif
 
+#ifndef LN_DRES_NT
+#define LN_DRES_NT 1  // the incoming residual gradient (written several kernels earlier): LN bwd 77.9 vs 79.1 us (profiles/ab/ln_dres_nt_r04.log)
+#endif
+
 namespace orion {
 
 template <typename T>
@@ -196,7 +200,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       if (EXACT || c < C) {
         xr[i] = ld_far(reinterpret_cast<const V*>(x + (size_t)rw * C + c));
         dyr[i] = *reinterpret_cast<const V*>(dy + (size_t)rw * C + c);
-        if (dres) rr[i] = *reinterpret_cast<const V*>(dres + (size_t)rw * C + c);
+        if (dres) {
+          if constexpr (LN_DRES_NT) rr[i] = ld_far(reinterpret_cast<const V*>(dres + (size_t)rw * C + c));
+          else rr[i] = *reinterpret_cast<const V*>(dres + (size_t)rw * C + c);
+        }
       }
     }
   };
