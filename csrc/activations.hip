@@ -128,6 +128,15 @@ __global__ __launch_bounds__(256) void scale_bf16_kernel(bf16_t* __restrict__ x,
 // the split-K weight gradient (S fp32 slabs from one launch over token chunks), with the
 // LM head's 1/n_valid * upstream-grad scale folded in.  out is the parameter's slice of
 // the gradient arena, fp32 (f32 != 0) or bf16.  Fixed summation order: deterministic.
+#ifndef SLAB_NT
+#define SLAB_NT 1  // 13.65 vs 14.1 us per call in the GPT-2 step (profiles/ab/slab_rmsdres_nt_r04.log)
+#endif
+// the slabs are read once, right after the weight-gradient kernel wrote them
+ORION_DEVICE f32x4 ld_slab(const f32x4* p) {
+  if constexpr (SLAB_NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slabs, int S,
                                                        long n4, void* __restrict__ out,
                                                        const float* __restrict__ scale,
@@ -139,12 +148,12 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
     // profiles/ab/slab_sum_unroll_r04.log)
     const f32x4* sp = reinterpret_cast<const f32x4*>(slabs) + i;
     const long sstride = n4;
-    f32x4 acc = sp[0];
+    f32x4 acc = ld_slab(sp);
     for (int k = 1; k < S; k += 8) {  // S is uniform: the guards are scalar branches
       f32x4 t[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (k + u < S) t[u] = sp[(k + u) * sstride];
+        if (k + u < S) t[u] = ld_slab(sp + (k + u) * sstride);
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (k + u < S) acc += t[u];

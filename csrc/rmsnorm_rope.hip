@@ -15,6 +15,9 @@
 // RMS_NT: the backward loads its saved input (read once, long after it was written) with the
 // non-temporal hint: rms_bwd 89.3 vs 93.8 us at Llama-7B shapes; the same on the forward's
 // residual stream measured neutral (profiles/ab/rms_nt_r04.log)
+#ifndef RMS_DRES_NT
+#define RMS_DRES_NT 1  // and the incoming residual gradient: rms_bwd 88.3 vs 89.4 us (profiles/ab/slab_rmsdres_nt_r04.log)
+#endif
 #ifndef RMS_NT
 #define RMS_NT 1
 #endif
@@ -133,7 +136,8 @@ __global__ __launch_bounds__(256) void rms_bwd_kernel(const bf16_t* __restrict__
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[i][j] - xh[i][j] * m);
         if (dres) {
           float rv[8];
-          ld8f(dres + (size_t)row * C + c, rv);
+          if constexpr (RMS_DRES_NT) ld8f<true>(dres + (size_t)row * C + c, rv);
+          else ld8f(dres + (size_t)row * C + c, rv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
