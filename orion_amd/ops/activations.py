@@ -180,27 +180,44 @@ class _FusedMLP(torch.autograd.Function):
         _notify(sbfc)
         dbfc = None if b_fc is None else _unless(dbfc, sbfc)
         grads = [None, None, None, None, None]
-        if ctx.needs_input_grad[3]:
-            if s_proj is not None:
-                wgrad_into(dy2, h, s_proj.view, s_proj.take())
-                s_proj.notify()
-            else:
-                grads[3] = wgrad(dy2, h)
-        if b_proj is not None and ctx.needs_input_grad[4]:
-            db = C().colsum(dy2, _view(sbproj))
-            grads[4] = None if sbproj is not None else db.to(b_proj.dtype)
-            _notify(sbproj)
-        if ctx.needs_input_grad[0]:
-            grads[0] = linear_dgrad(da, w_fc).view(ctx.x_shape)
-        if ctx.needs_input_grad[1]:
-            if s_fc is not None:
-                wgrad_into(da, x2, s_fc.view, s_fc.take())
-                s_fc.notify()
-            else:
-                grads[1] = wgrad(da, x2)
+
+        def proj_grads():
+            if ctx.needs_input_grad[3]:
+                if s_proj is not None:
+                    wgrad_into(dy2, h, s_proj.view, s_proj.take())
+                    s_proj.notify()
+                else:
+                    grads[3] = wgrad(dy2, h)
+            if b_proj is not None and ctx.needs_input_grad[4]:
+                db = C().colsum(dy2, _view(sbproj))
+                grads[4] = None if sbproj is not None else db.to(b_proj.dtype)
+                _notify(sbproj)
+
+        def fc_dgrad():
+            if ctx.needs_input_grad[0]:
+                grads[0] = linear_dgrad(da, w_fc).view(ctx.x_shape)
+
+        def fc_wgrad():
+            if ctx.needs_input_grad[1]:
+                if s_fc is not None:
+                    wgrad_into(da, x2, s_fc.view, s_fc.take())
+                    s_fc.notify()
+                else:
+                    grads[1] = wgrad(da, x2)
+        for step in {"0": (proj_grads, fc_dgrad, fc_wgrad), "1": (fc_dgrad, fc_wgrad, proj_grads),
+                     "2": (fc_wgrad, fc_dgrad, proj_grads)}[_MLP_BWD_ORDER]:
+            step()
         if dbfc is not None:
             grads[2] = dbfc.to(b_fc.dtype)
         return tuple(grads)
+
+
+# Order of the MLP backward's GEMMs after the fused GELU' one: 1 (default) = the fc input and
+# weight gradients first -- the two readers of da (403 MB at GPT-2's shape) back to back, while
+# it is still in the caches -- and the fc2 weight gradient / bias last; 0 = fc2 first (round 3);
+# 2 = fc weight gradient, fc input gradient, fc2.  GPT-2 step: 1 vs 0 +0.2 % (3 of 3), 2 vs 0
+# mixed (profiles/ab/mlp_bwd_order_r04.log).
+_MLP_BWD_ORDER = os.environ.get("ORION_MLP_BWD_ORDER", "1")
 
 
 def mlp_hip(x, w_fc, b_fc, w_proj, b_proj=None):
