@@ -231,6 +231,12 @@ def mlp_hip(x, w_fc, b_fc, w_proj, b_proj=None):
 _FUSED_SWIGLU = os.environ.get("ORION_FUSED_SWIGLU", "1") != "0"
 
 
+# Llama feed-forward backward order after the fused SwiGLU' GEMM, as _MLP_BWD_ORDER: here order
+# 1 measured neutral (dgu is 721 MB, larger than the caches: profiles/ab/mlp_bwd_order_r04.log),
+# so the default stays 0
+_SWIGLU_BWD_ORDER = os.environ.get("ORION_SWIGLU_BWD_ORDER", "0")
+
+
 def swiglu_mlp_ok(x, w_gu, w_down) -> bool:
     from .gemm import gemm16_addressable
     C_, F2 = x.shape[-1], w_gu.shape[0]
@@ -272,20 +278,30 @@ class _SwigluMLP(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         dgu = C().gemm_swiglu_bwd(dy2, w_down, gu)
         grads = [None, None, None]
-        if ctx.needs_input_grad[2]:
-            if s_down is not None:
-                wgrad_into(dy2, h, s_down.view, s_down.take())
-                s_down.notify()
-            else:
-                grads[2] = wgrad(dy2, h)
-        if ctx.needs_input_grad[0]:
-            grads[0] = linear_dgrad(dgu, w_gu).view(ctx.x_shape)
-        if ctx.needs_input_grad[1]:
-            if s_gu is not None:
-                wgrad_into(dgu, x2, s_gu.view, s_gu.take())
-                s_gu.notify()
-            else:
-                grads[1] = wgrad(dgu, x2)
+
+        def down_wgrad():
+            if ctx.needs_input_grad[2]:
+                if s_down is not None:
+                    wgrad_into(dy2, h, s_down.view, s_down.take())
+                    s_down.notify()
+                else:
+                    grads[2] = wgrad(dy2, h)
+
+        def gu_dgrad():
+            if ctx.needs_input_grad[0]:
+                grads[0] = linear_dgrad(dgu, w_gu).view(ctx.x_shape)
+
+        def gu_wgrad():
+            if ctx.needs_input_grad[1]:
+                if s_gu is not None:
+                    wgrad_into(dgu, x2, s_gu.view, s_gu.take())
+                    s_gu.notify()
+                else:
+                    grads[1] = wgrad(dgu, x2)
+        # the same orders as _FusedMLP (_SWIGLU_BWD_ORDER)
+        for step in {"0": (down_wgrad, gu_dgrad, gu_wgrad), "1": (gu_dgrad, gu_wgrad, down_wgrad),
+                     "2": (gu_wgrad, gu_dgrad, down_wgrad)}[_SWIGLU_BWD_ORDER]:
+            step()
         return tuple(grads)
 
 
