@@ -29,6 +29,10 @@
 #include "attn_params.h"
 #include "mfma_lds.h"
 
+#ifndef ATTN_FWD_QB64
+#define ATTN_FWD_QB64 2  // query blocks per wave at D = 64 (A/B builds: -DATTN_FWD_QB64=1)
+#endif
+
 namespace orion {
 
 // Plain fmaxf / + here: this file is built with -fno-honor-nans (no canonicalising
@@ -387,7 +391,7 @@ int orion_attn_fwd3(const AttnParams& p, int D, bool causal, hipStream_t st) {
   // softmax chains interleaved with each other's MFMAs; 255 VGPRs) -- equal in isolation to one
   // block per wave but faster in the whole GPT-2 step in 8 of 8 alternating pairs on two boxes
   // (+0.2-0.6 %, profiles/ab/ab_fwd_qb*.log); D = 128: one block per wave.
-  constexpr int qb64 = 2;
+  constexpr int qb64 = ATTN_FWD_QB64;
 #define FWD3(DD, CC) fwd3_launch<DD, CC>(p, qb64, lds, st);
   if (D == 64) {
     if (causal) { FWD3(64, true) } else { FWD3(64, false) }
