@@ -13,6 +13,13 @@ from ._ext import C
 from .gemm import WGRAD_FIRST, linear_dgrad, linear_fwd, wgrad, wgrad_into
 from .grad_sink import sink_of
 
+import os
+
+# LM head: weight gradient before the input gradient, so dX (read next by the final LayerNorm's
+# backward) is not evicted by the weight gradient's 6.6 GB pass over the logit gradient (A/B;
+# defaults to the global ORION_WGRAD_FIRST order)
+_LM_WGRAD_FIRST = os.environ.get("ORION_LMHEAD_WGRAD_FIRST", "1" if WGRAD_FIRST else "0") == "1"
+
 
 class _LinearXent(torch.autograd.Function):
     @staticmethod
@@ -28,7 +35,7 @@ class _LinearXent(torch.autograd.Function):
         x, w, dl = ctx.saved_tensors
         s = g.detach().float().reshape(1).contiguous()
         dx = dw = None
-        if ctx.needs_input_grad[0] and not WGRAD_FIRST:
+        if ctx.needs_input_grad[0] and not _LM_WGRAD_FIRST:
             dx = linear_dgrad(dl, w)
             C().scale_(dx, s)
         if ctx.needs_input_grad[1]:
@@ -38,7 +45,7 @@ class _LinearXent(torch.autograd.Function):
                 sink.notify()
             else:
                 dw = wgrad(dl, x, s)
-        if ctx.needs_input_grad[0] and WGRAD_FIRST:
+        if ctx.needs_input_grad[0] and _LM_WGRAD_FIRST:
             dx = linear_dgrad(dl, w)
             C().scale_(dx, s)
         return dx, dw, None, None
