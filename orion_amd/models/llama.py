@@ -143,7 +143,7 @@ class Llama(nn.Module):
     def forward(self, idx, targets=None, pos0=0):
         B, T = idx.shape
         assert pos0 + T <= self.config.max_seq_len
-        x = self.embed_tokens(idx)
+        x = ops.token_embedding(idx, self.embed_tokens.weight)
         cos, sin = self.rope_cos, self.rope_sin
         layers = self.layers
         h = layers[0].input_layernorm(x)

@@ -181,6 +181,16 @@ def embed_layer_norm(idx, wte, wpe, weight, bias, eps=1e-5):
     return x, layer_norm(x, weight, bias, eps)
 
 
+def token_embedding(idx, weight):
+    """weight[idx] (Llama's token embedding; ``embedding`` is the submodule's name).  On the GPU
+    the backward adds into the table's gradient-arena slice directly (ops/embedding.py)."""
+    b = _gpu(weight)
+    if b == "hip" and weight.shape[1] % 8 == 0 and weight.dtype == torch.bfloat16:
+        from .embedding import embedding_hip
+        return embedding_hip(idx, weight)
+    return F.embedding(idx, weight)
+
+
 def add_broadcast(x, pos):
     """x (B, T, C) + pos (T, C); kept as one op so the GPU path is one kernel."""
     return x + pos.to(x.dtype)
@@ -278,7 +288,8 @@ def linear_cross_entropy(x, weight, targets, ignore_index=-1):
 
 __all__ = [
     "set_backend", "backend", "ext_available", "load_ext",
-    "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm", "rope",
+    "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm",
+    "token_embedding", "rope",
     "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "swiglu_mlp",
     "linear_cross_entropy",
 ]
@@ -327,7 +338,8 @@ def _guarded(fn):
 
 
 for _name in ("layer_norm", "add_layer_norm", "add_rms_norm", "linear", "rms_norm", "bias_gelu",
-              "gelu_linear", "mlp", "swiglu_mlp", "embed_layer_norm", "add_broadcast", "linear_attention_qkv",
+              "gelu_linear", "mlp", "swiglu_mlp", "embed_layer_norm", "token_embedding", "add_broadcast",
+              "linear_attention_qkv",
               "linear_cross_entropy"):
     globals()[_name] = _guarded(globals()[_name])
 del _name
