@@ -181,11 +181,14 @@ def embed_layer_norm(idx, wte, wpe, weight, bias, eps=1e-5):
     return x, layer_norm(x, weight, bias, eps)
 
 
+_TORCH_EMBEDDING = os.environ.get("ORION_EMBEDDING") == "torch"  # A/B: PyTorch's embedding backward
+
+
 def token_embedding(idx, weight):
     """weight[idx] (Llama's token embedding; ``embedding`` is the submodule's name).  On the GPU
     the backward adds into the table's gradient-arena slice directly (ops/embedding.py)."""
     b = _gpu(weight)
-    if b == "hip" and weight.shape[1] % 8 == 0 and weight.dtype == torch.bfloat16:
+    if b == "hip" and weight.shape[1] % 8 == 0 and weight.dtype == torch.bfloat16 and not _TORCH_EMBEDDING:
         from .embedding import embedding_hip
         return embedding_hip(idx, weight)
     return F.embedding(idx, weight)
