@@ -77,7 +77,30 @@ def parse():
                          "next forward).  auto (default): on for models of >= 1B parameters at "
                          "N > 1 GPUs; a bare --zero1 = on (with one GPU: a world-1 rehearsal of "
                          "the sharded path)")
+    ap.add_argument("--per-item-walk", action="store_true",
+                    help="force gemm16's one-workgroup-per-item walk (what multi-rank training selects "
+                         "so RCCL kernels get CUs) also at N = 1: separates that walk's cost from the "
+                         "communication cost on a scaling curve")
+    ap.add_argument("--check-replicas", action="store_true",
+                    help="after the timed region, compare a checksum of every rank's full weights "
+                         "(and fp32 master) across ranks; reported as replicas_identical")
     return ap.parse_args()
+
+
+def _replica_checksums(trainer, dev):
+    """(bf16 compute weights, fp32 master) checksums of this rank's FULL model state: float64
+    sums of the values and of the values times a position ramp, so a permutation differs."""
+    if trainer.zero1:
+        trainer.reducer.wait_params()
+        master = trainer.full_master()
+    else:
+        master = trainer.opt.master
+    out = []
+    for t in (trainer.arena.params, master):
+        v = t.detach().double()
+        ramp = torch.arange(v.numel(), device=v.device, dtype=torch.float64) / max(1, v.numel())
+        out += [float(v.sum()), float((v * ramp).sum())]
+    return torch.tensor(out, device=dev, dtype=torch.float64)
 
 
 def _per_item_walk() -> bool:
@@ -154,6 +177,9 @@ def main():
                           grad_dtype=torch.float32 if args.grad_dtype == "fp32" else torch.bfloat16,
                           ddp_timing=world > 1, zero1={"auto": None, "on": True, "off": False}[args.zero1])
         step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
+        if args.per_item_walk and dev.type == "cuda":
+            from orion_amd.ops.gemm import set_per_item_walk
+            set_per_item_walk(True)
     else:
         ddp_model = model
         if world > 1:
@@ -208,7 +234,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     final_loss = float(loss)
-    busbw = ddp = rccl = None
+    busbw = ddp = rccl = replicas = None
+    if args.check_replicas and args.impl == "native":
+        mine = _replica_checksums(trainer, dev)
+        if world > 1:
+            allc = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(allc, mine)
+        else:
+            allc = [mine]
+        replicas = {"identical": all(torch.equal(c, allc[0]) for c in allc),
+                    "checksums": [round(float(x), 6) for x in allc[0].tolist()]}
     if world > 1 and args.impl == "native":
         # bucket timeline of the last timed step: launch -> complete per bucket, exposed tail
         ddp = trainer.reducer.timing_report()
@@ -268,6 +303,7 @@ def main():
             "allreduce_busbw_gbps": busbw,
             "ddp_buckets": ddp,
             "rccl": rccl,
+            "replicas": replicas,
             "config": {"model": f"{args.model} ({n_params / 1e6:.1f}M params)",
                        "global_batch": B * A * world, "micro_batch": B, "grad_accum": A,
                        "seq_len": T, "tokens_per_step": B * T * A * world,

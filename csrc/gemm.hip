@@ -45,9 +45,10 @@ static int gemm_diag() {
   return g_diag;
 }
 
+// flags < 0: query only
 int orion_gemm_set_diag(int flags) {
   const int old = gemm_diag();
-  g_diag = flags < 0 ? 0 : flags;
+  if (flags >= 0) g_diag = flags;
   return old;
 }
 

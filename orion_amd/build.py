@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import shlex
 import subprocess
@@ -78,24 +79,35 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     for src in sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + [os.path.join(CSRC, "bindings.cpp")]:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
-        stale = force or not os.path.exists(obj) or \
+        base = bind if src.endswith(".cpp") else kern
+        name = os.path.basename(src)
+        extra = FILE_FLAGS.get(name, [])
+        # A/B builds: ORION_AMD_FLAGS_<STEM> (e.g. ORION_AMD_FLAGS_XENT) adds flags to one
+        # source; ORION_AMD_ATTN_FLAGS to both attention sources
+        extra = extra + os.environ.get("ORION_AMD_FLAGS_" + name.split(".")[0].upper(), "").split()
+        if name.startswith("attn_"):
+            extra = extra + os.environ.get("ORION_AMD_ATTN_FLAGS", "").split()
+        cmd = base + extra + ["-c", src, "-o", obj]
+        # the effective command is part of the staleness check: an object built with A/B
+        # flags is rebuilt by the next default build (and vice versa), not kept by mtime
+        stamp = obj + ".cmd"
+        sig = hashlib.sha256("\0".join(cmd).encode()).hexdigest()
+        same_cmd = os.path.exists(stamp) and open(stamp).read().strip() == sig
+        stale = force or not same_cmd or not os.path.exists(obj) or \
             os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_time)
         if stale:
-            base = bind if src.endswith(".cpp") else kern
-            name = os.path.basename(src)
-            extra = FILE_FLAGS.get(name, [])
-            # A/B builds: ORION_AMD_FLAGS_<STEM> (e.g. ORION_AMD_FLAGS_XENT) adds flags to one
-            # source; ORION_AMD_ATTN_FLAGS to both attention sources
-            extra = extra + os.environ.get("ORION_AMD_FLAGS_" + name.split(".")[0].upper(), "").split()
-            if name.startswith("attn_"):
-                extra = extra + os.environ.get("ORION_AMD_ATTN_FLAGS", "").split()
-            jobs_list.append(base + extra + ["-c", src, "-o", obj])
+            if os.path.exists(stamp):
+                os.remove(stamp)
+            jobs_list.append((cmd, stamp, sig))
     jobs = jobs or min(8, os.cpu_count() or 4)
     if jobs_list:
         with cf.ThreadPoolExecutor(jobs) as ex:
-            futs = [ex.submit(_run, c, verbose) for c in jobs_list]
+            futs = [ex.submit(_run, c, verbose) for c, _, _ in jobs_list]
             for f in futs:
                 f.result()
+        for _, stamp, sig in jobs_list:
+            with open(stamp, "w") as fh:
+                fh.write(sig + "\n")
     newest_obj = max(os.path.getmtime(o) for o in objs)
     if force or jobs_list or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest_obj:
         tlib = libdirs[0]

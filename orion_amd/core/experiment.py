@@ -30,9 +30,13 @@ from __future__ import annotations
 
 import copy
 import datetime
+import errno
 import getpass
 import logging
+import os
 import random
+import socket
+import uuid
 from dataclasses import dataclass
 
 from ..space.dsl import ScriptTemplate
@@ -151,14 +155,21 @@ class Experiment:
 
     # ------------------------------------------------------------------ trial budget
     # Trials that count toward ``max_trials``: every status but ``broken``.  The experiment
-    # document carries ``budget = {"used": n, "t": time of the last change}``, the number of
-    # such trials registered or about to be; a producer takes tokens with a compare-and-swap
-    # on it BEFORE inserting trials, a broken trial gives its token back, so concurrent
-    # producers can never register more than ``max_trials`` counting trials (the reference
-    # counted, then inserted: W workers overshot by up to W x pool_size,
-    # src/orion/core/worker/producer.py:35-45).
+    # document carries ``budget = {"used": n, "v": version, "t": time, "claims": {...}}``:
+    # ``used`` counts the counting trials registered or about to be; a producer takes tokens
+    # with a compare-and-swap on the version BEFORE it inserts, as a CLAIM recorded under a
+    # fresh claim id with its owner (host, pid, worker) and stage; it inserts its trials under
+    # ids derived from the claim id, then settles the claim (gives back what it did not
+    # insert, removes the record).  So concurrent producers can never register more than
+    # ``max_trials`` counting trials (the reference counted, then inserted: W workers
+    # overshot by up to W x pool_size, src/orion/core/worker/producer.py:35-45), a claim of a
+    # producer that died is recovered exactly (its inserted trials are found by id), and a
+    # settle after such a recovery is a no-op (no double release).
     LIVE_STATI = ("new", "reserved", "suspended", "interrupted", "completed")
     BUDGET_ATTEMPTS = 256
+    # a claim whose owner cannot be probed (another host) is presumed dead after this long by
+    # the writer's clock; owners on this host are probed by pid and recovered only when dead
+    CLAIM_FOREIGN_GRACE_S = 3600.0
 
     def _budgeted(self):
         return self.max_trials not in (None, float("inf")) and self._id is not None
@@ -167,36 +178,103 @@ class Experiment:
         docs = self._db.read("experiments", {"_id": self._id}, selection={"budget": 1})
         return docs[0].get("budget") if docs else None
 
-    def _budget_cas(self, old, used):
+    def _budget_cas(self, old, used, claims=None):
+        """Replace the budget document if it is still ``old`` (compared by version; documents
+        from before the version field by ``used`` and ``t``)."""
         q = {"_id": self._id}
         if old is None:
             q["budget"] = {"$exists": False}
+            v = 1
+        elif "v" in old:
+            q["budget.v"] = old["v"]
+            v = int(old["v"]) + 1
         else:
             q["budget.used"], q["budget.t"] = old["used"], old["t"]
-        return self._db.read_and_write("experiments", q, {"budget": {"used": int(used), "t": utcnow()}}) is not None
+            v = 1
+        if claims is None:
+            claims = dict((old or {}).get("claims") or {})
+        new = {"used": int(used), "v": v, "t": utcnow(), "claims": claims}
+        return self._db.read_and_write("experiments", q, {"budget": new}) is not None
 
-    def claim_budget(self, n):
-        """Take up to ``n`` registration tokens; returns how many were taken (0 when the budget
-        is spent).  Unbudgeted experiments (``max_trials`` infinite) always get ``n``."""
-        if n <= 0:
-            return 0
-        if not self._budgeted():
-            return n
-        for _ in range(self.BUDGET_ATTEMPTS):
+    def _seeded_budget(self):
+        b = self._budget_doc()
+        if b is None:  # first use (or an experiment from before the counter): seed it
+            self._budget_cas(None, self.count_trials(self.LIVE_STATI), {})
             b = self._budget_doc()
-            if b is None:  # first use (or an experiment from before the counter): seed it
-                self._budget_cas(None, self.count_trials(self.LIVE_STATI))
+        return b
+
+    @staticmethod
+    def claim_trial_id(cid, i):
+        """The id of the ``i``-th trial inserted under budget claim ``cid``."""
+        return f"{cid}.{i}"
+
+    def take_budget(self, n, owner=None):
+        """Take up to ``n`` registration tokens as a recorded claim: returns ``(k, cid)``, ``k``
+        tokens (0 when the budget is spent) under claim id ``cid`` (None for an unbudgeted
+        experiment, which always gets ``n``)."""
+        if n <= 0:
+            return 0, None
+        if not self._budgeted():
+            return n, None
+        for _ in range(self.BUDGET_ATTEMPTS):
+            b = self._seeded_budget()
+            if b is None:
                 continue
             k = min(n, int(self.max_trials) - int(b["used"]))
             if k <= 0:
-                return 0
-            if self._budget_cas(b, int(b["used"]) + k):
-                return k
+                return 0, None
+            cid = uuid.uuid4().hex
+            claims = dict(b.get("claims") or {})
+            claims[cid] = {"n": int(k), "host": socket.gethostname(), "pid": os.getpid(),
+                           "owner": owner, "t": utcnow(), "stage": "suggest"}
+            if self._budget_cas(b, int(b["used"]) + k, claims):
+                return k, cid
         log.warning("trial budget: no token after %d attempts (heavy contention)", self.BUDGET_ATTEMPTS)
-        return 0
+        return 0, None
+
+    def _update_claim(self, cid, fn):
+        """Apply ``fn(budget, claim) -> (used, claim or None) | None`` to claim ``cid`` under
+        the compare-and-swap; returns False when the claim no longer exists."""
+        for _ in range(self.BUDGET_ATTEMPTS):
+            b = self._budget_doc()
+            claims = dict((b or {}).get("claims") or {})
+            if cid not in claims:
+                return False
+            r = fn(b, claims[cid])
+            if r is None:
+                return True
+            used, c = r
+            if c is None:
+                claims.pop(cid)
+            else:
+                claims[cid] = c
+            if self._budget_cas(b, used, claims):
+                return True
+        return False
+
+    def confirm_claim(self, cid):
+        """Mark claim ``cid`` as inserting; False when it was recovered meanwhile (its owner was
+        presumed dead), in which case the caller must not insert its trials."""
+        if cid is None:
+            return True
+        return self._update_claim(cid, lambda b, c: (int(b["used"]), dict(c, stage="insert")))
+
+    def settle_budget(self, cid, inserted):
+        """Close claim ``cid`` after ``inserted`` of its trials were registered: the rest of its
+        tokens go back.  A no-op when the claim was already recovered."""
+        if cid is None:
+            return
+        self._update_claim(cid, lambda b, c: (max(0, int(b["used"]) - (int(c["n"]) - int(inserted))), None))
+
+    def claim_budget(self, n):
+        """Anonymous tokens (no claim record): up to ``n``; see :meth:`take_budget`."""
+        k, cid = self.take_budget(n)
+        if cid is not None:
+            self._update_claim(cid, lambda b, c: (int(b["used"]), None))
+        return k
 
     def release_budget(self, k):
-        """Give back ``k`` tokens (a suggestion shortfall, a failed insert, a broken trial)."""
+        """Give back ``k`` anonymous tokens (a broken trial, an unclaimed shortfall)."""
         if k <= 0 or not self._budgeted():
             return
         for _ in range(self.BUDGET_ATTEMPTS):
@@ -206,20 +284,44 @@ class Experiment:
             if self._budget_cas(b, max(0, int(b["used"]) - k)):
                 return
 
-    def reconcile_budget(self, grace_s=60.0):
-        """A producer that died between taking tokens and inserting its trials leaks them:
-        when the counter has not moved for ``grace_s`` and exceeds the counting trials that
-        exist, set it back to that count.  Returns the number of tokens recovered."""
+    @classmethod
+    def _claim_owner_dead(cls, c, now, grace_s):
+        if c.get("host") == socket.gethostname() and c.get("pid"):
+            try:
+                os.kill(int(c["pid"]), 0)
+            except OSError as e:
+                return e.errno == errno.ESRCH
+            return False
+        t = c.get("t")
+        return t is not None and now - t > datetime.timedelta(seconds=grace_s)
+
+    def reconcile_budget(self, grace_s=None):
+        """Recover the tokens of claims whose producer died between taking them and settling:
+        an owner on this host is dead when its pid is gone; an owner on another host is
+        presumed dead after ``grace_s`` (default :attr:`CLAIM_FOREIGN_GRACE_S`).  A recovered
+        claim gives back exactly the tokens its trials (found by their claim-derived ids) do
+        not hold.  Returns the number of tokens recovered."""
         if not self._budgeted():
             return 0
+        grace_s = self.CLAIM_FOREIGN_GRACE_S if grace_s is None else grace_s
         b = self._budget_doc()
-        if b is None or utcnow() - b["t"] < datetime.timedelta(seconds=grace_s):
-            return 0
-        live = self.count_trials(self.LIVE_STATI)
-        if live < int(b["used"]) and self._budget_cas(b, live):
-            log.warning("trial budget: recovered %d token(s) leaked by a dead producer", int(b["used"]) - live)
-            return int(b["used"]) - live
-        return 0
+        now = utcnow()
+        dead = [cid for cid, c in ((b or {}).get("claims") or {}).items()
+                if self._claim_owner_dead(c, now, grace_s)]
+        got = 0
+        for cid in dead:
+            def fn(b, c, cid=cid):
+                ids = [self.claim_trial_id(cid, i) for i in range(int(c["n"]))]
+                found = self._db.count("trials", {"experiment": self._id, "_id": {"$in": ids},
+                                                  "status": {"$in": list(self.LIVE_STATI)}})
+                back = int(c["n"]) - found
+                fn.back = back
+                return max(0, int(b["used"]) - back), None
+            fn.back = 0
+            if self._update_claim(cid, fn) and fn.back:
+                log.warning("trial budget: recovered %d token(s) of claim %s (producer dead)", fn.back, cid)
+                got += fn.back
+        return got
 
     def register_trials(self, trials):
         stamp = utcnow()

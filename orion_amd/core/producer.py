@@ -38,24 +38,35 @@ class Producer:
             n = min(n, int(max_trials) - live)
         return max(0, n)
 
-    def produce(self):
+    def produce(self, owner=None):
         """Register up to ``pool_size`` suggestions, never past ``max_trials``: the tokens are
-        taken with a compare-and-swap on the experiment's budget counter before the insert,
-        and whatever is not inserted is given back."""
-        claim = getattr(self.experiment, "claim_budget", None)
-        n = claim(self.num_new_trials) if claim else self.budget()
+        taken as a recorded claim on the experiment's budget counter (compare-and-swap) before
+        the algorithm is asked, the trials are inserted under claim-derived ids once the claim
+        is confirmed, and whatever is not inserted is given back when the claim is settled."""
+        take = getattr(self.experiment, "take_budget", None)
+        if take is not None:
+            n, cid = take(self.num_new_trials, owner)
+        else:
+            n, cid = self.budget(), None
         if n <= 0:
             return 0
         inserted = 0
         try:
             points = self.algorithm.suggest(n) or []
             trials = [format_trials.tuple_to_trial(p, self.space) for p in points[:n]]
+            if cid is not None:
+                if not self.experiment.confirm_claim(cid):
+                    log.warning("budget claim %s was recovered while suggesting; dropping %d point(s)",
+                                cid, len(trials))
+                    return 0
+                for i, t in enumerate(trials):
+                    t._id = self.experiment.claim_trial_id(cid, i)
             log.debug("registering %d new trial(s)", len(trials))
             self.experiment.register_trials(trials)
             inserted = len(trials)
         finally:
-            if claim and inserted < n:
-                self.experiment.release_budget(n - inserted)
+            if cid is not None:
+                self.experiment.settle_budget(cid, inserted)
         return inserted
 
     def update(self):

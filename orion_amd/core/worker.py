@@ -61,7 +61,7 @@ def _workon(experiment, consumer, max_broken, idle_sleep):
             experiment.fix_lost_trials(stale_after)
             experiment.reconcile_budget()
             if (experiment.count_trials(("new", "suspended", "interrupted")) == 0
-                    and producer.produce() > 0):
+                    and producer.produce(owner=worker_id) > 0):
                 sleep = idle_sleep[0]
             else:
                 time.sleep(sleep)

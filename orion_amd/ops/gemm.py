@@ -104,11 +104,15 @@ def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
 _PER_ITEM = False
 
 
-def set_per_item_walk(on: bool) -> None:
-    """Select gemm16's one-workgroup-per-item walk (True) or the persistent walk (False)."""
+def set_per_item_walk(on: bool) -> bool:
+    """Select gemm16's one-workgroup-per-item walk (True) or the persistent walk (False).
+    Only the walk bit (64) of the diagnostic flags changes; returns the previous setting."""
     global _PER_ITEM
+    prev = _PER_ITEM
     _PER_ITEM = bool(on)
-    C().gemm_diag(64 if _PER_ITEM else 0)
+    cur = C().gemm_diag(-1)  # query
+    C().gemm_diag((cur | 64) if _PER_ITEM else (cur & ~64))
+    return prev
 
 
 def per_item_walk() -> bool:

@@ -339,6 +339,10 @@ class ShardedGradReducer(GradBucketReducer):
         self._pgather = [None] * len(self.buckets)
         self.overlap_gather = os.environ.get("ORION_ZERO1_OVERLAP", "1") != "0"
         self._hooks = []
+        # ORION_ZERO1_CHECK=1 (debug): the first gradient of a step asserts that the forward
+        # waited for every overlapped weight gather -- an op that read weights outside the
+        # module pre-hooks and the ops param guard would otherwise read last step's weights
+        self.check_gathers = os.environ.get("ORION_ZERO1_CHECK") == "1"
 
     # the fused AdamW (train/optim.py) takes this object as its "arena": flat params (the
     # bf16 shard it writes), grads (the reduced fp32 shard), decay flags and the initial fp32
@@ -390,6 +394,14 @@ class ShardedGradReducer(GradBucketReducer):
             if keep:
                 full[b0:b1].copy_(tmp[:b1 - b0])
         return full
+
+    def _on_grad(self, p):
+        if self.check_gathers and self._sync and not any(self._arrived):
+            pend = [bi for bi, h in enumerate(self._pgather) if h is not None]
+            if pend:
+                raise RuntimeError(f"ZeRO-1: the weight gathers of buckets {pend} were not waited "
+                                   "for before the backward (an op read weights unguarded)")
+        super()._on_grad(p)
 
     def _launch(self, bi):
         if self._handles[bi] is not None:

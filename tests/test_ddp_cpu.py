@@ -183,6 +183,39 @@ def test_bench_spawns_its_own_ranks_on_cpu(zero1):
     assert rec["zero1"] == zero1
 
 
+@pytest.mark.parametrize("model", ["gpt2-tiny", "llama-tiny"])
+@pytest.mark.parametrize("zero1", ["off", "on"])
+def test_bench_eight_ranks_on_cpu(model, zero1):
+    """The driver's N = 8 job rehearsed on the CPU: ``bench.py --gpus 8``
+    self-spawns 8 gloo ranks; every gradient bucket of the last step is launched in order and
+    completes after it was ready, and after the timed steps every rank holds bit-identical
+    weights and fp32 master (replicated: all-reduce; ZeRO-1: reduce-scatter + all-gather)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in
+           ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--model", model,
+                          "--device", "cpu", "--dist-backend", "gloo", "--seq-len", "64",
+                          "--micro-batch", "2", "--steps", "2", "--warmup", "1", "--bucket-mb", "0.25",
+                          "--zero1", zero1, "--check-replicas", "--no-busbw"],
+                         cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8"
+    assert rec["zero1"] == (zero1 == "on")
+    ddp = rec["ddp_buckets"]
+    assert ddp is not None and len(ddp["buckets"]) > 2
+    assert [b[0] for b in ddp["buckets"]] == list(range(len(ddp["buckets"])))
+    assert all(done >= ready for _, _, ready, done in ddp["buckets"])
+    assert ddp["exposed_tail_ms_max_over_ranks"] >= ddp["exposed_tail_ms"] >= 0
+    assert rec["replicas"]["identical"], rec["replicas"]
+
+
 def test_default_bucket_size_by_model_size():
     from orion_amd.parallel.ddp import default_bucket_mb
     assert default_bucket_mb(124_000_000) == 64.0

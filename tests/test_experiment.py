@@ -252,3 +252,71 @@ def test_plan_configuration_is_pure(storage):
     copy_cfg["metadata"]["user_args"] = ["-x~uniform(0, 2)"]
     with pytest.raises(NotImplementedError, match="metadata"):
         plan_configuration(plan.config, other)
+
+
+# ---------------------------------------------------------------- budget claims
+def test_slow_suggest_keeps_its_claim(storage, monkeypatch):
+    """A producer whose suggest outlasts any grace period keeps its tokens: its owner (this
+    process) is alive, so reconcile recovers nothing and the budget never overshoots."""
+    exp = _ready(storage, max_trials=3, pool_size=2)
+    prod = Producer(exp)
+    orig = prod.algorithm.suggest
+    other = Producer(exp)
+
+    nested = []
+
+    def slow_suggest(n):
+        # while this claim is open: an aggressive reconcile (grace 0) and a second producer
+        # (which shares the algorithm object, hence the guard)
+        if not nested:
+            nested.append(1)
+            assert exp.reconcile_budget(grace_s=0.0) == 0
+            assert other.produce() == 1  # only 3 - 2 tokens are left
+        return orig(n)
+
+    monkeypatch.setattr(prod.algorithm, "suggest", slow_suggest)
+    assert prod.produce() == 2
+    assert exp.count_trials("new") == 3
+    b = storage.read("experiments", {"_id": exp.id})[0]["budget"]
+    assert b["used"] == 3 and b["claims"] == {}
+    assert Producer(exp).produce() == 0
+
+
+def test_dead_producer_claim_is_recovered(storage):
+    import subprocess
+    import sys
+    exp = _ready(storage, max_trials=4, pool_size=4)
+    k, cid = exp.take_budget(3, owner="dead")
+    assert k == 3
+    # the claim's owner: a process that has exited
+    p = subprocess.Popen([sys.executable, "-c", "pass"])
+    p.wait()
+    b = storage.read("experiments", {"_id": exp.id})[0]["budget"]
+    b["claims"][cid]["pid"] = p.pid
+    storage.write("experiments", {"budget": b}, {"_id": exp.id})
+    # it inserted one of its three trials before dying
+    t = Trial(params=[dict(name="/x", type="real", value=1.0)])
+    t._id = exp.claim_trial_id(cid, 0)
+    exp.register_trials([t])
+    assert exp.reconcile_budget() == 2
+    b = storage.read("experiments", {"_id": exp.id})[0]["budget"]
+    assert b["used"] == 1 and b["claims"] == {}
+    assert Producer(exp).produce() == 3
+
+
+def test_settle_after_recovery_is_a_noop(storage):
+    """A foreign-host claim presumed dead after the grace period is recovered once; when its
+    producer turns out to be alive, its confirm fails (it inserts nothing) and its settle
+    gives nothing back twice."""
+    exp = _ready(storage, max_trials=4, pool_size=2)
+    k, cid = exp.take_budget(2, owner="far")
+    b = storage.read("experiments", {"_id": exp.id})[0]["budget"]
+    b["claims"][cid]["host"] = "some-other-host"
+    b["claims"][cid]["t"] = utcnow() - datetime.timedelta(hours=2)
+    storage.write("experiments", {"budget": b}, {"_id": exp.id})
+    assert exp.reconcile_budget() == 2
+    assert storage.read("experiments", {"_id": exp.id})[0]["budget"]["used"] == 0
+    assert not exp.confirm_claim(cid)
+    exp.settle_budget(cid, 0)
+    assert storage.read("experiments", {"_id": exp.id})[0]["budget"]["used"] == 0
+    assert exp.take_budget(9)[0] == 4

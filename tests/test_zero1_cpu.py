@@ -178,3 +178,28 @@ def test_zero1_overlapped_gather_matches_serial(world):
     for rank, same_params, same_master, nhooks in res:
         assert same_params and same_master, rank
         assert nhooks > 0
+
+
+def test_zero1_check_catches_an_unwaited_gather(monkeypatch):
+    """ORION_ZERO1_CHECK=1: with the module pre-hooks and the ops param guard gone, a forward
+    reads weights whose overlapped gather is still pending; the first gradient of the backward
+    reports it instead of the step silently using last step's weights."""
+    monkeypatch.setenv("ORION_ZERO1_CHECK", "1")
+    port = _free_port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    from orion_amd.parallel.launch import init_process_group
+    init_process_group("gloo")
+    try:
+        g = torch.Generator().manual_seed(2)
+        data = [(torch.randint(0, 50257, (2, 32), generator=g), torch.randint(0, 50257, (2, 32), generator=g))]
+        tr = _trainer(True, 0.05)
+        assert tr.reducer.check_gathers
+        tr.step(data)  # guarded: fine
+        for h in tr.reducer._hooks:
+            h.remove()
+        tr.reducer._remove_guard()
+        tr.reducer.gather_params(overlap=True)
+        with pytest.raises(RuntimeError, match="not waited"):
+            tr.step(data)
+    finally:
+        dist.destroy_process_group()
