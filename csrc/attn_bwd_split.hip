@@ -9,9 +9,10 @@
 // The split recomputes S and dP once more (7 instead of 5 matmuls per (q, key) pair) but
 // each kernel keeps its accumulators and operand fragments in registers:
 //
-//   delta          delta[q] = sum_d dO O: a separate HBM-bound pass (default), or computed
-//                  by the dq kernel from its dO fragments and written for the kv kernel
-//                  launched after it (ORION_ATTN_DELTA=fused)
+//   delta          delta[q] = sum_d dO O: a separate HBM-bound pass (computing it inside the
+//                  dQ kernel measured 0.3 % slower end to end -- its extra O loads sit in the
+//                  prologue ahead of the first K/V tile -- and was removed in round 5;
+//                  profiles/ab/ab_attn_delta.log)
 //   kv kernel      per workgroup 32*NW keys, loop over 32-row query tiles (and the query
 //                  heads of its KV head):  S = Q K^T, dP = dO V^T (key on the lane, V
 //                  fragments in registers, K in registers or an LDS image),
@@ -479,11 +480,7 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 // tile advance in the scalar offset, the tile loop unrolled over the two LDS buffers (every
 // LDS address a per-lane register plus an immediate), the causal / length mask one
 // compare + select per score against a per-lane bound.
-// FUSE_DELTA: the kernel computes delta = rowsum(dO O) of its own queries from the dO
-// fragments it holds anyway plus the matching half-row of O (one more 16-byte load per
-// k-step, the halves joined by one lane exchange), and writes it for the dK/dV kernel,
-// which is then launched after this one: no separate delta pass over O and dO.
-template <int D, bool CAUSAL, bool FUSE_DELTA, bool BIAS = false>
+template <int D, bool CAUSAL, bool BIAS = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
@@ -515,20 +512,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
     }
     const long r = ((long)b * p.Hq + hq) * p.T + qr;
     L = p.lse[r];
-    if constexpr (FUSE_DELTA) {
-      const bf16_t* Or = p.o + b * p.o_sb + hq * p.o_sh + (long)qr * p.o_st;
-      float sd = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(Or + ks * 16 + 8 * h32);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sd = fmaf(bf2f(ov[j]), bf2f(df[ks][j]), sd);
-      }
-      dl = sd + __shfl_xor(sd, 32, 64);  // the other half of the row
-      if (h32 == 0 && myq < p.T) const_cast<float*>(p.delta)[r] = dl;
-    } else {
-      dl = p.delta[r];
-    }
+    dl = p.delta[r];
   }
   const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
   const int ntiles = (kend + BN - 1) / BN;
@@ -676,33 +660,19 @@ static void kv_launch(const AttnParams& q, int grid, hipStream_t st) {
   attn_bwd_kv_kernel<D, CAUSAL><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
 }
 
-template <int D, bool CAUSAL, bool FUSE, bool BIAS = false>
+template <int D, bool CAUSAL, bool BIAS = false>
 static void dq_launch(const AttnParams& q, int grid, hipStream_t st) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, FUSE, BIAS>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, BIAS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
     done = true;
   }
-  attn_bwd_dq_kernel<D, CAUSAL, FUSE, BIAS><<<grid, 256, dq_lds(D), st>>>(q);
-}
-
-// ORION_ATTN_DELTA=fused: delta computed inside the dQ kernel (launched first); default: the
-// separate delta pass.  Fused measured 0.3 % SLOWER end to end (1,004.2k vs 1,007.4k tok/s, four
-// alternating runs, profiles/ab/ab_attn_delta.log): the dQ kernel's extra O loads sit in its
-// prologue, ahead of the first K/V tile, which costs more than the 35 us HBM-bound pass.
-static bool delta_fused() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ORION_ATTN_DELTA");
-    v = (e && strcmp(e, "fused") == 0) ? 1 : 0;
-  }
-  return v == 1;
+  attn_bwd_dq_kernel<D, CAUSAL, BIAS><<<grid, 256, dq_lds(D), st>>>(q);
 }
 
 // delta (caller-allocated [B][Hq][T] fp32 scratch), dK/dV and dQ; p.dq / dk / dv are bf16
-// outputs (strided views allowed).  Default order: delta pass, dK/dV, dQ; with
-// ORION_ATTN_DELTA=fused: dQ (computing and writing delta), then dK/dV (reading it).
+// outputs (strided views allowed).  Order: delta pass, dK/dV, dQ.
 int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
   // 32-bit buffer offsets: the dQ kernel addresses one (batch, KV head)'s K / V, the dK/dV
   // kernel one batch's Q / dO over all query heads; beyond 2 GB the caller takes the fused
@@ -718,7 +688,6 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   q.delta = delta;
   const int kv_grid = ((p.Tk + 32 * 4 - 1) / (32 * 4)) * p.B * p.Hkv;
   const int dq_grid = ((p.T + 127) / 128) * p.B * p.Hq;
-  const bool fused = delta_fused();
   static const bool diag = getenv("ORION_ATTN_DIAG") && getenv("ORION_ATTN_DIAG")[0] == '1';
   if (diag && D == 64) {  // stamped dK/dV kernel only, stamps over p.dq (scripts/attn_stamps.py)
     attn_delta_kernel<64><<<pre_grid, 256, 0, st>>>(p, delta);
@@ -734,24 +703,19 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
     return (int)hipGetLastError();
   }
   if (p.bias_part) {  // packed self-attention with the QKV bias gradient (GPT-2: D = 64, MHA)
-    if (D != 64 || fused || p.T != p.Tk || p.Hq != p.Hkv || p.T % 32) return -3;
+    if (D != 64 || p.T != p.Tk || p.Hq != p.Hkv || p.T % 32) return -3;
 #define SPLITB(CC)                                                                                  \
   attn_delta_kernel<64, true><<<pre_grid, 256, 0, st>>>(q, delta);                                  \
   kv_launch<64, CC>(q, kv_grid, st);                                                                \
-  dq_launch<64, CC, false, true>(q, dq_grid, st);
+  dq_launch<64, CC, true>(q, dq_grid, st);
     if (causal) { SPLITB(true) } else { SPLITB(false) }
 #undef SPLITB
     return (int)hipGetLastError();
   }
-#define SPLIT(DD, CC)                                                                   \
-  if (fused) {                                                                          \
-    dq_launch<DD, CC, true>(q, dq_grid, st);                                            \
-    kv_launch<DD, CC>(q, kv_grid, st);                                                  \
-  } else {                                                                              \
-    attn_delta_kernel<DD><<<pre_grid, 256, 0, st>>>(p, delta);                          \
-    kv_launch<DD, CC>(q, kv_grid, st);                                                  \
-    dq_launch<DD, CC, false>(q, dq_grid, st);                                           \
-  }
+#define SPLIT(DD, CC)                                    \
+  attn_delta_kernel<DD><<<pre_grid, 256, 0, st>>>(p, delta); \
+  kv_launch<DD, CC>(q, kv_grid, st);                       \
+  dq_launch<DD, CC>(q, dq_grid, st);
   if (D == 64) {
     if (causal) { SPLIT(64, true) } else { SPLIT(64, false) }
   } else if (D == 128) {

@@ -787,10 +787,11 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
 }
 
 // Backward form: "split" (csrc/attn_bwd_split.hip: dK/dV and dQ kernels, no atomics,
-// deterministic) or "fused" (csrc/attention.hip: one pass, fp32-atomic dQ).  Split is the
-// default (MI355X: 0.632 vs 0.722 ms at B64 T1024 H12 D64, 3.39 vs 4.46 ms at B4 T4096
-// H32/8 D128); flags bit 2 (deterministic) forces split, bit 3 forces fused; otherwise
-// ORION_ATTN_BWD = split | v1 | v2 overrides the default.
+// deterministic) always, except for operands whose 32-bit buffer offsets overflow (one batch's
+// Q / dO or one KV head's K / V beyond 2 GB): those take the 64-bit-addressed fused kernel of
+// csrc/attention.hip (one pass, fp32-atomic dQ; split measured faster wherever both run:
+// 0.632 vs 0.722 ms at B64 T1024 H12 D64, 3.39 vs 4.46 ms at B4 T4096 H32/8 D128).  flags bit 2
+// (deterministic) forces split; bit 3 forces the large-operand fallback (its test only).
 // column sums of the packed bf16 dQKV starting at dq ([rows][ld], contiguous)
 void attn_bias_colsum_packed(const Tensor& dq, const Tensor& out, long rows, long ld) {
   auto part = at::empty({(long)orion_colsum_scratch((int)rows, (int)ld)}, dq.options().dtype(at::kFloat));
@@ -801,14 +802,7 @@ void attn_bias_colsum_packed(const Tensor& dq, const Tensor& out, long rows, lon
 
 bool attn_bwd_use_split(int D, int64_t flags) {
   if (flags & 4) return true;
-  if (flags & 8) return false;  // force the fused form (A/B tests)
-  static int env = -1;  // -1 unread, 0 none, 1 split, 2 fused
-  if (env < 0) {
-    const char* e = getenv("ORION_ATTN_BWD");
-    env = !e ? 0 : (strcmp(e, "split") == 0 ? 1 : 2);
-  }
-  if (env) return env == 1;
-  return true;  // measured faster at both head dims (docs/PERFORMANCE.md)
+  return !(flags & 8);  // bit 3: the large-operand fallback's test
 }
 
 // dq/dk/dv: preallocated outputs (may be strided views of one packed buffer)

@@ -1,4 +1,6 @@
-"""Flash-attention autograd wrappers over csrc/attention.hip.
+"""Flash-attention autograd wrappers over the HIP kernels: csrc/attn_fwd.hip (forward) and
+csrc/attn_bwd_split.hip (delta, dK/dV and dQ kernels, the backward); csrc/attention.hip keeps
+the 64-bit-addressed forms for operands beyond the others' 32-bit buffer offsets.
 
 ``flash_attention_qkv`` consumes the packed (B, T, 3C) output of a fused QKV
 projection through strided views and produces the packed gradient in one

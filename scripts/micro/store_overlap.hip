@@ -91,12 +91,17 @@ __global__ __launch_bounds__(256, 2) void kern(const unsigned short* __restrict_
         u32x4 pk;
         for (int e = 0; e < 4; ++e) pk[e] = __float_as_uint(acc[k & 7][(k >> 3) * 2][e]) ^ __float_as_uint(acc[k & 7][(k >> 3) * 2 + 1][e]);
         const unsigned off = (unsigned)((m - m0) * N * 2 + nw * 2 + c0 + colb_l);
-        if (flags & 0x2000) {
-          __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, 2);
-          __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off, 0, 2);
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off, 0, 0);
+        // cache-policy bits of the stores ((flags >> 12) & 7): 0 none, 1 nt (aux 2), 2 sc1 (16),
+        // 3 nt | sc1 (18), 4 sc0 (1), 5 sc0 | nt (3)
+        switch ((flags >> 12) & 7) {
+#define ST(AUX) __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, AUX); __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off, 0, AUX); break;
+          case 1: ST(2)
+          case 2: ST(16)
+          case 3: ST(18)
+          case 4: ST(1)
+          case 5: ST(3)
+          default: ST(0)
+#undef ST
         }
       }
       t_store += __builtin_amdgcn_s_memtime() - ts;
@@ -137,20 +142,19 @@ int main(int argc, char** argv) {
   const int tiles = (M / 128) * (N / 256);
   std::vector<Cfg> cfgs;
   const char* pn[7] = {"1 row x 1 KB", "", "4 rows x 256 B", "8 rows x 128 B", "16 rows x 64 B (gemm16)", "", "64 rows x 16 B"};
+  const char* an[6] = {"plain", "nt", "sc1", "nt|sc1", "sc0", "sc0|nt"};
   static char names[64][96];
   int ni = 0;
-  for (int lr : {4, 3, 2, 0, 6}) {
-    for (int base : {2, 3, 11}) {
-      snprintf(names[ni], 96, "%s %s", base == 2 ? "MFMA+stores" : base == 3 ? "MFMA+DMA+stores" : "MFMA+DMA+stores deferred", pn[lr]);
-      cfgs.push_back({names[ni++], 512, base | (lr << 8)});
-    }
-  }
-  snprintf(names[ni], 96, "MFMA+DMA+stores deferred, 8 rows x 128 B, nt");
-  cfgs.push_back({names[ni++], 512, 11 | (3 << 8) | (2 << 12)});
   snprintf(names[ni], 96, "MFMA+DMA (no stores)");
   cfgs.push_back({names[ni++], 512, 1});
-  snprintf(names[ni], 96, "MFMA only");
-  cfgs.push_back({names[ni++], 512, 0});
+  for (int lr : {4, 3, 0}) {
+    for (int a : {0, 1, 2, 3, 4, 5}) {
+      snprintf(names[ni], 96, "MFMA+DMA+stores deferred %s %s", pn[lr], an[a]);
+      cfgs.push_back({names[ni++], 512, 11 | (lr << 8) | (a << 12)});
+    }
+  }
+  snprintf(names[ni], 96, "MFMA+DMA (no stores)");
+  cfgs.push_back({names[ni++], 512, 1});
   std::vector<unsigned long> hc(1024 * 8);
   for (int rep = 0; rep < 1; ++rep) {
     for (auto& c : cfgs) {
