@@ -87,6 +87,23 @@ ORION_DEVICE G16Item g16_decode(const GemmArgs& g, int w) {
 #ifndef G16_PRE_NT
 #define G16_PRE_NT 1  // GPT-2 step: the fc2 / attn-proj forwards that read the GELU output next 166 -> 156 us (profiles/ab/gemm16_pre_nt_r04.log)
 #endif
+// Epilogue store shape (round 5).  Each lane holds 16 bytes (8 consecutive n) of one row after
+// the permlane16_swap, so a plain store instruction covers 16 rows x 64 B.  G16_WIDE_ST = 1:
+// a DPP row_ror:8 exchange between the packed results of two adjacent column pairs makes it
+// 8 rows x 128 B (whole 128-byte lines): one store instruction touches half as many rows.
+// Microbenchmark (scripts/micro/store_overlap.hip, profiles/micro_store_pattern_r05.log): with
+// two workgroups per CU streaming LDS-DMA beside the stores, 16 x 64 B cost +0.14 ms over
+// no stores, 8 x 128 B +0.09, 1 x 1 KB +0.03.
+#ifndef G16_WIDE_ST
+#define G16_WIDE_ST 1
+#endif
+// cache-policy bits of the second output (GELU activation / dup) and of plain outputs: nt (2).
+// Same box, 2 rounds each (profiles/ab/gemm16_wide_nt_r05.log): LM-head forward 5.39-5.43 ms
+// (16 x 64 B stores) -> 5.03 (8 x 128 B) -> 4.28-4.30 (8 x 128 B, nt; hipBLASLt 3.86); GPT-2
+// step 1,119.9-1,124.0k -> 1,126.6-129.0k -> 1,136.1-1,137.2k tok/s.
+#ifndef G16_ST_AUX
+#define G16_ST_AUX 2
+#endif
 
 // The epilogue of one work item (registers only, no LDS).
 template <int EPI>
@@ -174,6 +191,7 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
   };
   [[maybe_unused]] u32x4 preA[4], preB[4], upA[4], upB[4];
   if constexpr (PRE) load_pre(0, preA, upA);
+  [[maybe_unused]] u32x4 parkA[4], parkB[4];  // G16_WIDE_ST: packed results of the even pair
   // the value arithmetic runs on pairs of adjacent columns (v_pk_*_f32: no MFMA issues beside
   // the epilogue) and every pair is packed to bf16 by one v_cvt_pk_bf16_f32
 #pragma unroll
@@ -228,22 +246,63 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
           v[e] = v[e] * uu * fma2(gg * sg, splat2(1.f) - sg, sg);
         }
       }
-      const bool ok = m < g.M && nok;
-      const unsigned off = ok ? (unsigned)(((long)(m - m0) * g.ldo + nb) * 2) : 0xFFFFFFF0u;
-      u32x4 pk;
+      u32x4 pk, pk2;
 #pragma unroll
       for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(v[e]);
-      // bias + GELU: the pre-activation is read again only by the backward -- streamed past
-      // the caches (G16_PRE_NT)
-      __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, (EPI == EPI_BIAS_GELU && G16_PRE_NT) ? 2 : 0);
       if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
-        const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if constexpr (EPI == EPI_BIAS_GELU) pk[e] = pack2_bf16(gelu_x2(v[e]));
-          else pk[e] = pack2_bf16(du[e]);
+          if constexpr (EPI == EPI_BIAS_GELU) pk2[e] = pack2_bf16(gelu_x2(v[e]));
+          else pk2[e] = pack2_bf16(du[e]);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(pk, ro2, off2, 0, 0);
+      }
+      // bias + GELU: the pre-activation is read again only by the backward -- streamed past
+      // the caches (G16_PRE_NT)
+      constexpr int AUX1 = (EPI == EPI_BIAS_GELU && G16_PRE_NT) ? 2 : G16_ST_AUX;
+      if constexpr (G16_WIDE_ST) {
+        // even column pair: park; odd pair: exchange lane bit 3 (row i16 & 8) with the pair
+        // index, so that store 0 covers rows 0-7 and store 1 rows 8-15 of this 16-row group,
+        // each over both pairs' 32 + 32 columns (8 rows x 128 B)
+        if ((ap & 1) == 0) {
+          parkA[b] = pk;
+          if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) parkB[b] = pk2;
+        } else {
+          const int hi = (i16 >> 3) & 1;
+          auto xchg = [&](const u32x4& a, const u32x4& bb, u32x4& n0, u32x4& n1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              // row_ror:8 (dpp_ctrl 0x128) reads lane i16 ^ 8; banks 2-3 are lanes 8-15 of a row
+              n0[e] = (unsigned)__builtin_amdgcn_update_dpp((int)a[e], (int)bb[e], 0x128, 0xF, 0xC, false);
+              n1[e] = (unsigned)__builtin_amdgcn_update_dpp((int)bb[e], (int)a[e], 0x128, 0xF, 0x3, false);
+            }
+          };
+          u32x4 n0, n1;
+          xchg(parkA[b], pk, n0, n1);
+          // after the exchange lane (q, i16) holds column pair ap - 1 + hi of rows
+          // 16 b + (i16 & 7) (n0) and 16 b + 8 + (i16 & 7) (n1)
+          const int ncx = nw + 16 * (2 * (ap - 1 + hi) + (q & 1)) + 8 * (q >> 1);
+          const int mr0 = mw + 16 * b + (i16 & 7), mr1 = mr0 + 8;
+          const bool nx = ncx < g.N;
+          const unsigned o0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo + ncx) * 2) : 0xFFFFFFF0u;
+          const unsigned o1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo + ncx) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_buffer_store_b128(n0, ro, o0, 0, AUX1);
+          __builtin_amdgcn_raw_buffer_store_b128(n1, ro, o1, 0, AUX1);
+          if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
+            xchg(parkB[b], pk2, n0, n1);
+            const unsigned p0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
+            const unsigned p1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
+            __builtin_amdgcn_raw_buffer_store_b128(n0, ro2, p0, 0, G16_ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(n1, ro2, p1, 0, G16_ST_AUX);
+          }
+        }
+      } else {
+        const bool ok = m < g.M && nok;
+        const unsigned off = ok ? (unsigned)(((long)(m - m0) * g.ldo + nb) * 2) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, AUX1);
+        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
+          const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_buffer_store_b128(pk2, ro2, off2, 0, G16_ST_AUX);
+        }
       }
       if constexpr (CS) {
         const f32x2 keep = splat2(m < g.M ? 1.f : 0.f);  // rows past M repeat row M - 1
