@@ -59,6 +59,13 @@ int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, vo
                const void*, void*, long, const void*, long, hipStream_t, void* db = nullptr,
                int db_f32 = 0, float* part = nullptr);
 int orion_gemm_colsum_scratch(int M, int N);
+int orion_gemm_lm(const void*, long, const void*, long, int, int, int, int, void*, long, float*,
+                  const int64_t*, float*, const float*, const float*, hipStream_t);
+int orion_lmhead_fold(const float*, int, const float*, const int64_t*, long, float*, void*, long, int, long,
+                      const void*, long, const void*, long, int, float*, float*, float*, int*, int*, float*,
+                      float*, hipStream_t);
+int orion_lmhead_bwd_prep(const void*, long, int, long, const int64_t*, long, int, const float*, const float*,
+                          const float*, float*, void*, hipStream_t);
 int orion_gemm_set_diag(int flags);
 
 namespace {
@@ -398,6 +405,83 @@ void scale_(Tensor x, const Tensor& s) {
 
 // ------------------------------------------------------------------ cross entropy
 // logits (N, V) bf16 contiguous -> overwritten with dlogits/n_valid; returns fp32 loss (scalar)
+// LM head + cross-entropy without the logits pass (csrc/lmhead.hip): x (N, C), w (V, C) bf16,
+// targets (N,) int64, cref a one-element fp32 device tensor (the running exp reference, updated
+// in place).  Returns the mean loss, E' (N, V) bf16 (exp(logit - ref) with the one-hot term
+// folded in), invz (N,) = 1 / Z per row and inv_n (1,) = 1 / n_valid.
+std::tuple<Tensor, Tensor, Tensor, Tensor> lmhead_fwd(const Tensor& x, const Tensor& w, const Tensor& targets,
+                                                      int64_t ignore_index, Tensor cref) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "lmhead_fwd: x must be (N, C) with unit column stride");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == x.size(1), "lmhead_fwd: w must be a contiguous (V, C)");
+  TORCH_CHECK(targets.scalar_type() == at::kLong && targets.numel() == x.size(0), "lmhead_fwd: targets (N,) int64");
+  TORCH_CHECK(cref.scalar_type() == at::kFloat && cref.numel() == 1 && cref.is_cuda(), "lmhead_fwd: cref fp32 (1,)");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const long N = x.size(0);
+  const int Cd = (int)x.size(1), V = (int)w.size(0);
+  TORCH_CHECK(N < (1L << 31) && V % 8 == 0 && Cd % 64 == 0, "lmhead_fwd: unsupported shape");
+  auto t = targets.contiguous();
+  auto fopts = x.options().dtype(at::kFloat);
+  auto E = at::empty({N, (long)V}, x.options());
+  const int npart = (V + 127) / 128;
+  auto part = at::empty({N * npart}, fopts);
+  auto tlog = at::empty({N}, fopts);
+  auto invz = at::empty({N}, fopts);
+  auto lse = at::empty({N}, fopts);
+  auto lrow = at::empty({N}, fopts);
+  auto ints = at::empty({4 + N}, x.options().dtype(at::kInt));
+  auto loss = at::empty({}, fopts);
+  auto inv_n = at::empty({1}, fopts);
+  check_launch(orion_gemm_lm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), (int)N, V, Cd, 6, E.data_ptr(),
+                             V, part.data_ptr<float>(), t.data_ptr<int64_t>(), tlog.data_ptr<float>(),
+                             cref.data_ptr<float>(), nullptr, cur_stream()),
+               "lmhead_fwd gemm");
+  check_launch(orion_lmhead_fold(part.data_ptr<float>(), npart, tlog.data_ptr<float>(), t.data_ptr<int64_t>(),
+                                 ignore_index, cref.data_ptr<float>(), E.data_ptr(), V, V, N, x.data_ptr(),
+                                 x.stride(0), w.data_ptr(), w.stride(0), Cd, invz.data_ptr<float>(),
+                                 lse.data_ptr<float>(), lrow.data_ptr<float>(), ints.data_ptr<int>(),
+                                 ints.data_ptr<int>() + 4, loss.data_ptr<float>(), inv_n.data_ptr<float>(),
+                                 cur_stream()),
+               "lmhead_fold");
+  return {loss, E, invz, inv_n};
+}
+
+// Backward prologue: srow (N,) fp32 = g / (Z n_valid) on valid rows, xs (N, C) = srow (.) x.
+std::tuple<Tensor, Tensor> lmhead_bwd_prep(const Tensor& x, const Tensor& targets, int64_t ignore_index,
+                                           int64_t V, const Tensor& invz, const Tensor& inv_n, const Tensor& g) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "lmhead_bwd_prep: x (N, C)");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(x.device());
+  const long N = x.size(0);
+  const int Cd = (int)x.size(1);
+  auto t = targets.contiguous();
+  auto srow = at::empty({N}, x.options().dtype(at::kFloat));
+  auto xs = at::empty({N, (long)Cd}, x.options());
+  auto gf = g.to(at::kFloat).reshape({1}).contiguous();
+  check_launch(orion_lmhead_bwd_prep(x.data_ptr(), x.stride(0), Cd, N, t.data_ptr<int64_t>(), ignore_index, (int)V,
+                                     invz.data_ptr<float>(), inv_n.data_ptr<float>(), gf.data_ptr<float>(),
+                                     srow.data_ptr<float>(), xs.data_ptr(), cur_stream()),
+               "lmhead_bwd_prep");
+  return {srow, xs};
+}
+
+// dx (N, C) = srow (.) (e . w): the LM head's input gradient from E' (N, V) and w (V, C).
+Tensor gemm_rowscale(const Tensor& e, const Tensor& w, const Tensor& srow) {
+  check_bf16(e, "e");
+  check_bf16(w, "w");
+  TORCH_CHECK(e.dim() == 2 && e.stride(1) == 1 && w.dim() == 2 && w.is_contiguous() && w.size(0) == e.size(1),
+              "gemm_rowscale: e (N, V), w (V, C)");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(e.device());
+  const long N = e.size(0);
+  const int V = (int)e.size(1), Cd = (int)w.size(1);
+  auto out = at::empty({N, (long)Cd}, e.options());
+  check_launch(orion_gemm_lm(e.data_ptr(), e.stride(0), w.data_ptr(), w.stride(0), (int)N, Cd, V, 7, out.data_ptr(),
+                             Cd, nullptr, nullptr, nullptr, nullptr, srow.data_ptr<float>(), cur_stream()),
+               "gemm_rowscale");
+  return out;
+}
+
 Tensor xent_fwd_bwd(Tensor logits, const Tensor& targets, int64_t ignore_index) {
   check_bf16(logits, "logits");
   TORCH_CHECK(logits.is_contiguous() && logits.dim() == 2, "logits must be contiguous (N, V)");
@@ -937,6 +1021,9 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("wgrad_splits(int M, int N1, int N2) -> int", &wgrad_splits);  // host-only helper
   m.def("gemm_diag(int flags) -> int", &gemm_diag);                   // host-only helper
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
+  m.def("lmhead_fwd(Tensor x, Tensor w, Tensor targets, int ignore_index, Tensor(a!) cref) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("lmhead_bwd_prep(Tensor x, Tensor targets, int ignore_index, int V, Tensor invz, Tensor inv_n, Tensor g) -> (Tensor, Tensor)");
+  m.def("gemm_rowscale(Tensor e, Tensor w, Tensor srow) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");
   m.def("gemm_swiglu_bwd(Tensor dy, Tensor w, Tensor gate_up) -> Tensor");
@@ -968,6 +1055,9 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("wgrad", &wgrad);
   m.impl("wgrad_into", &wgrad_into);
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
+  m.impl("lmhead_fwd", &lmhead_fwd);
+  m.impl("lmhead_bwd_prep", &lmhead_bwd_prep);
+  m.impl("gemm_rowscale", &gemm_rowscale);
   m.impl("gemm", &gemm);
   m.impl("gemm_gelu_bwd", &gemm_gelu_bwd);
   m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);

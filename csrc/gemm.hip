@@ -85,3 +85,29 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   if (rc == 0 && db) rc = orion_colsum_partials2(part, part + (long)rows * N, db, rows, N, db_f32, st);
   return rc;
 }
+
+// LM head (csrc/lmhead.hip): the forward GEMM with the exp epilogue (epi = EPI_EXP, NT W
+// [N][K]: row partial sums into rowpart[M][npart = ceil(N / 128)], the target logits into
+// tlog) and the input-gradient GEMM with the per-row scale (epi = EPI_ROWSCALE, W [K][N]).
+int orion_gemm_lm(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, int epi,
+                  void* out, long ldo, float* rowpart, const int64_t* tgt, float* tlog, const float* cref,
+                  const float* rs, hipStream_t st) {
+  if (M < 1 || K < 64 || K % 64 || N % 8 || N < 8) return -1;
+  if ((ldx | ldw | ldo) % 8) return -1;
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
+       reinterpret_cast<uintptr_t>(out)) & 15) return -2;
+  if (epi == EPI_EXP && (!rowpart || !tgt || !tlog || !cref)) return -3;
+  if (epi == EPI_ROWSCALE && !rs) return -3;
+  if (epi != EPI_EXP && epi != EPI_ROWSCALE) return -3;
+  GemmArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)out, ldo,
+             nullptr, nullptr, 0, nullptr, 0, M, N, K, (N + 255) / 256, gemm_diag()};
+  a.rowpart = rowpart;
+  a.npart = (N + 127) / 128;
+  a.tgt = tgt;
+  a.tlog = tlog;
+  a.cref = cref;
+  a.rs = rs;
+  const int wkm = epi == EPI_ROWSCALE ? 1 : 0;
+  if (!gemm16_ok(a, wkm)) return -1;
+  return gemm16(a, wkm, epi, st);
+}

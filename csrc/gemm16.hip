@@ -192,6 +192,26 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
   [[maybe_unused]] u32x4 preA[4], preB[4], upA[4], upB[4];
   if constexpr (PRE) load_pre(0, preA, upA);
   [[maybe_unused]] u32x4 parkA[4], parkB[4];  // G16_WIDE_ST: packed results of the even pair
+  // LM head: the lane's four rows' targets / scales, the exp reference, row-sum accumulators
+  constexpr float L2E = 1.4426950408889634f;
+  [[maybe_unused]] int tg[4];
+  [[maybe_unused]] float rsb[4], rsum[4];
+  [[maybe_unused]] f32x2 cl2;
+  if constexpr (EPI == EPI_EXP || EPI == EPI_ROWSCALE) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int mc = min(mw + 16 * b + i16, g.M - 1);
+      if constexpr (EPI == EPI_EXP) {
+        const long t = g.tgt[mc];
+        tg[b] = (t >= 0 && t < g.N) ? (int)t : -1;
+        rsum[b] = 0.f;
+      } else {
+        rsb[b] = g.rs[mc];
+      }
+    }
+    if constexpr (EPI == EPI_EXP) cl2 = splat2(-*g.cref * L2E);
+  }
+
   // the value arithmetic runs on pairs of adjacent columns (v_pk_*_f32: no MFMA issues beside
   // the epilogue) and every pair is packed to bf16 by one v_cvt_pk_bf16_f32
 #pragma unroll
@@ -205,6 +225,7 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
         else load_pre(ap + 1, preB, upB);
       }
     }
+
     [[maybe_unused]] f32x2 bias[4];
     if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_GELU_BWD) {
 #pragma unroll
@@ -234,6 +255,29 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       if constexpr (EPI == EPI_GELU_BWD) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] *= gelu_grad_x2(unpack2(p4[e]) + bias[e]);
+      }
+      if constexpr (EPI == EPI_EXP) {
+        // the target's logit (fp32, before the exp) for the loss; exp(acc - cref) and its row sum
+        const int d = tg[b] - nb;
+        if (d >= 0 && d < 8 && m < g.M) {
+          float tl = 0.f;  // v[d >> 1][d & 1] without a runtime register index (scratch)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if ((d >> 1) == e) tl = (d & 1) ? v[e].y : v[e].x;
+          g.tlog[m] = tl;
+        }
+        f32x2 se = splat2(0.f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x2 z = fma2(v[e], splat2(L2E), cl2);
+          v[e] = f32x2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)};
+          se += v[e];
+        }
+        if (nok) rsum[b] += se.x + se.y;
+      }
+      if constexpr (EPI == EPI_ROWSCALE) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= splat2(rsb[b]);
       }
       [[maybe_unused]] f32x2 du[4];
       if constexpr (EPI == EPI_SWIGLU_BWD) {
@@ -339,6 +383,17 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
         const int n = nb + ((i16 >> 1) & 7);
         if (!(i16 & 1) && mw < g.M && n < g.N) g.colsum[(long)(mw / 64) * g.N + n] = tot;
       }
+    }
+  }
+  if constexpr (EPI == EPI_EXP) {
+    // the four q lanes of a row hold its 128 columns: fold them, one partial per (row, wave)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      float r = rsum[b];
+      r += __shfl_xor(r, 16);
+      r += __shfl_xor(r, 32);
+      const int m = mw + 16 * b + i16;
+      if (q == 0 && m < g.M) g.rowpart[(long)m * g.npart + nw / 128] = r;
     }
   }
 }
@@ -714,6 +769,8 @@ int gemm16(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
     case EPI_BIAS_GELU * 2 + 0: return gemm16_launch<false, false, EPI_BIAS_GELU>(a, st);
     case EPI_GELU_BWD * 2 + 1: return gemm16_launch<false, true, EPI_GELU_BWD>(a, st);
     case EPI_SWIGLU_BWD * 2 + 1: return gemm16_launch<false, true, EPI_SWIGLU_BWD>(a, st);
+    case EPI_EXP * 2 + 0: return gemm16_launch<false, false, EPI_EXP>(a, st);
+    case EPI_ROWSCALE * 2 + 1: return gemm16_launch<false, true, EPI_ROWSCALE>(a, st);
     default: return -4;
   }
 }

@@ -7,7 +7,7 @@
 namespace orion {
 
 enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3, EPI_WGRAD = 4,
-               EPI_SWIGLU_BWD = 5 };
+               EPI_SWIGLU_BWD = 5, EPI_EXP = 6, EPI_ROWSCALE = 7 };
 
 struct GemmArgs {
   const bf16_t* X;  long ldx;   // [M][K] row-major
@@ -29,6 +29,15 @@ struct GemmArgs {
   // EPI_GELU_BWD: fp32 column sums of the result (the bias gradient)
   // per 64-row block, colsum[ceil(M / 64)][N]; null = none
   float* colsum;
+  // LM head + cross-entropy (csrc/lmhead.hip).  EPI_EXP (forward, NT): out = exp(acc - *cref)
+  // (bf16), rowpart[m][n / 128] = fp32 sum of those over the wave's 128 columns, tlog[m] =
+  // acc at column tgt[m].  EPI_ROWSCALE (input gradient): out = rs[m] acc (the softmax's
+  // 1 / Z per row; the one-hot term is folded into the exp tile by the fold kernel).
+  float* rowpart; int npart;
+  const int64_t* tgt;
+  float* tlog;
+  const float* cref;
+  const float* rs;
 };
 
 // ---- 16x16x32 kernel helpers (csrc/gemm16.hip)

@@ -1,9 +1,13 @@
-"""Fused softmax-cross-entropy wrappers over csrc/xent.hip.
+"""Fused softmax-cross-entropy wrappers.
 
-``linear_cross_entropy`` fuses the LM head: logits = x W^T (hipBLASLt GEMM),
-then one kernel computes the loss AND writes dlogits over the logits buffer,
-so backward is two GEMMs on the saved dlogits with the upstream gradient
-applied to the small (N, C) / (V, C) results.
+``linear_cross_entropy`` fuses the LM head.  Default (``ORION_LMHEAD=exp``,
+csrc/lmhead.hip): the in-tree forward GEMM writes E = exp(logits - ref) with
+per-row partial sums and the target logits from its epilogue, a fold over the
+partials gives the loss and folds the one-hot term into E, and the backward is
+dX = s (E W) (row scale in the GEMM epilogue) and dW = E^T (s X) -- no pass over
+the (tokens x vocab) buffer besides the three GEMMs.  ``ORION_LMHEAD=rowpass``:
+round 4's form, logits = x W^T (hipBLASLt) then one kernel (csrc/xent.hip)
+computes the loss and writes dlogits over the logits buffer.
 """
 from __future__ import annotations
 
@@ -53,7 +57,61 @@ class _LinearXent(torch.autograd.Function):
 
 def linear_cross_entropy_hip(x, w, targets, ignore_index=-1):
     """mean cross-entropy of softmax(x @ w^T) against targets; x (N, C), w (V, C)."""
+    if lmhead_exp_eligible(x, w):
+        return _LinearXentExp.apply(x, w, targets, ignore_index)
     return _LinearXent.apply(x, w, targets, ignore_index)
+
+
+_LMHEAD = os.environ.get("ORION_LMHEAD", "exp")
+_CREF = {}
+
+
+def _cref(dev):
+    """The running exp reference of the LM-head forward on ``dev`` (a device scalar the fold
+    kernel updates: the largest row log-sum-exp of the previous call)."""
+    t = _CREF.get(dev)
+    if t is None:
+        t = _CREF[dev] = torch.zeros(1, dtype=torch.float32, device=dev)
+    return t
+
+
+def lmhead_exp_eligible(x, w) -> bool:
+    return (_LMHEAD == "exp" and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.dim() == 2 and x.stride(1) == 1 and w.is_contiguous() and x.shape[1] % 64 == 0
+            and w.shape[0] % 64 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0
+            and w.data_ptr() % 16 == 0 and x.shape[0] % 32 == 0)
+
+
+class _LinearXentExp(torch.autograd.Function):
+    """LM head + cross-entropy through the exp-epilogue GEMM (csrc/lmhead.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, w, targets, ignore_index):
+        t = targets.contiguous()
+        loss, e, invz, inv_n = C().lmhead_fwd(x, w, t, int(ignore_index), _cref(x.device))
+        ctx.save_for_backward(x, w, t, e, invz, inv_n)
+        ctx.ignore = int(ignore_index)
+        ctx.sink = sink_of(w)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, t, e, invz, inv_n = ctx.saved_tensors
+        srow, xs = C().lmhead_bwd_prep(x, t, ctx.ignore, w.shape[0], invz, inv_n, g.detach())
+        one = torch.ones(1, dtype=torch.float32, device=x.device)
+        dx = dw = None
+        if ctx.needs_input_grad[0] and not _LM_WGRAD_FIRST:
+            dx = C().gemm_rowscale(e, w, srow)
+        if ctx.needs_input_grad[1]:
+            sink = ctx.sink
+            if sink is not None:
+                wgrad_into(e, xs, sink.view, sink.take(), one)
+                sink.notify()
+            else:
+                dw = wgrad(e, xs, one)
+        if ctx.needs_input_grad[0] and _LM_WGRAD_FIRST:
+            dx = C().gemm_rowscale(e, w, srow)
+        return dx, dw, None, None
 
 
 class _Xent(torch.autograd.Function):
