@@ -4,7 +4,9 @@ csrc/gemm16.hip (with its fused epilogues) vs hipBLASLt through PyTorch (committ
 table loaded) plus the separate HIP epilogue kernels it needs.  Interleaved rounds in one
 process, median per variant; one JSON line per shape.
 
-usage: python scripts/bench_gemm.py [--M 65536] [--iters 20] [--check]
+usage: python scripts/bench_gemm.py [--M 65536] [--iters 20] [--check] [--cfgs p,s,w,o]
+(cfgs: p gemm16 persistent, s one workgroup per item, w gemmp two workgroups per CU, o gemmp
+with the second workgroup of a CU started half an item late)
 """
 import argparse
 import json
@@ -56,13 +58,13 @@ def main():
     # (name, kind, N, K, epi): fwd = x (M,K) . W(N,K)^T; dgrad = dy (M,K) . W(K,N)
     shapes = [("qkv_fwd", "fwd", 2304, 768, 1), ("attnproj_fwd", "fwd", 768, 768, 0),
               ("fc_fwd+bias+gelu", "fwd", 3072, 768, 2), ("mlpproj_fwd", "fwd", 768, 3072, 0),
-              ("lmhead_fwd", "fwd", 50304, 768, 0),
+              ("lmhead_fwd", "fwd", 50304, 768, 0), ("lmhead_exp", "fwd", 50304, 768, 6),
               ("qkv_dgrad", "dgrad", 768, 2304, 0), ("attnproj_dgrad", "dgrad", 768, 768, 0),
               ("fc_dgrad", "dgrad", 768, 3072, 0), ("mlpproj_dgrad+gelu_bwd", "dgrad", 3072, 768, 3),
               # 5: gemm_gelu_bwd (GELU'(pre + b) and the bias gradient in the epilogue) against
               # the unfused dgrad GEMM + bias_gelu_bwd (which also sums the bias gradient)
               ("mlpproj_dgrad+gelu_bwd+db", "dgrad", 3072, 768, 5),
-              ("lmhead_dgrad", "dgrad", 768, 50304, 0)]
+              ("lmhead_dgrad", "dgrad", 768, 50304, 0), ("lmhead_dgrad_rowscale", "dgrad", 768, 50304, 7)]
     if a.llama:
         shapes = [("l_qkv_fwd", "fwd", 12288, 4096, 0), ("l_o_fwd", "fwd", 4096, 4096, 0),
                   ("l_gateup_fwd", "fwd", 22016, 4096, 0), ("l_down_fwd", "fwd", 4096, 11008, 0),
@@ -85,12 +87,21 @@ def main():
         w = rnd(N, K) if kind == "fwd" else rnd(K, N)
         b = rnd(N) if epi in (1, 2, 5) else None
         pre = rnd(M, N) if epi in (3, 5) else None
-        if kind == "fwd":
+        if epi == 6:  # LM head: exp epilogue + fold (csrc/lmhead.hip) vs hipBLASLt logits
+            tg = torch.randint(0, N, (M,), device="cuda", generator=g)
+            cref = torch.zeros(1, device="cuda")
+            hip = lambda: ops.lmhead_fwd(x, w, tg, -1, cref)
+            blas = lambda: torch.nn.functional.linear(x, w)
+        elif kind == "fwd":
             hip = lambda: ops.gemm(x, w, False, epi, b, None)
             if epi == 2:
                 blas = lambda: ops.bias_gelu_fwd(torch.nn.functional.linear(x, w), b)
             else:
                 blas = lambda: torch.nn.functional.linear(x, w, b)
+        elif epi == 7:  # LM head input gradient with the per-row softmax scale in the epilogue
+            srow = torch.rand(M, device="cuda", generator=g)
+            hip = lambda: ops.gemm_rowscale(x, w, srow)
+            blas = lambda: x @ w
         else:
             hip = lambda: ops.gemm(x, w, True, epi, None, pre)
             if epi == 5:
@@ -103,7 +114,7 @@ def main():
                 blas = lambda: x @ w
         def with_cfg(c, f):
             def run():
-                ops.gemm_diag({"s": 64}.get(c, 0))
+                ops.gemm_diag({"s": 64, "w": 0x2000, "o": 0x3000}.get(c, 0))
                 return f()
             return run
         fns = {f"hip{c}": with_cfg(c, hip) for c in cfgs}
@@ -116,7 +127,7 @@ def main():
                "hip_TFs": round(flop / t["hip"] / 1e9, 1), "blas_TFs": round(flop / t["blas"] / 1e9, 1)}
         for c in cfgs[1:]:
             rec[f"cfg{c}_TFs"] = round(flop / t[f"hip{c}"] / 1e9, 1)
-        if a.check:
+        if a.check and epi not in (6, 7):
             ref = (x.float() @ (w.float().t() if kind == "fwd" else w.float()))
             if b is not None and epi != 5:
                 ref = ref + b.float()
