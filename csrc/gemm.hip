@@ -81,8 +81,7 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   if (!gemm16_ok(a, wkm)) return -1;
   const int rows = (M + 63) / 64;
   if (db) a.colsum = part;
-  // flags & 0x2000: the two-workgroups-per-CU kernel (gemmp) instead of gemm16
-  int rc = (a.flags & 0x2000) ? gemmp(a, wkm, epi, st) : gemm16(a, wkm, epi, st);
+  int rc = gemm16(a, wkm, epi, st);
   if (rc == 0 && db) rc = orion_colsum_partials2(part, part + (long)rows * N, db, rows, N, db_f32, st);
   return rc;
 }
@@ -110,5 +109,5 @@ int orion_gemm_lm(const void* X, long ldx, const void* W, long ldw, int M, int N
   a.rs = rs;
   const int wkm = epi == EPI_ROWSCALE ? 1 : 0;
   if (!gemm16_ok(a, wkm)) return -1;
-  return (a.flags & 0x2000) ? gemmp(a, wkm, epi, st) : gemm16(a, wkm, epi, st);
+  return gemm16(a, wkm, epi, st);
 }

@@ -722,269 +722,6 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   }
 }
 
-// =============================================================================================
-// gemmp: TWO workgroups per CU (round 5), for the short-K GEMMs whose epilogue gemm16 serialises.
-//
-// gemm16 runs one 8-wave workgroup per CU; after an item's last MFMA all eight waves run the
-// epilogue (VALU + stores) while the matrix pipe idles, and the next item's first LDS-DMA wait
-// also waits for those stores (CDNA4's vmcnt retires in issue order, stores included): at
-// K = 768 with two outputs (fc + bias + GELU) the epilogue is ~1/3 of the item.  Here a
-// workgroup is 4 waves (one per SIMD) with a 72 KB LDS plan, so two run on every CU and one's
-// epilogue runs beside the other's main loop (scripts/micro/store_overlap.hip: stores hidden
-// beside a co-resident workgroup's MFMA + LDS-DMA stream when they are issued as whole lines
-// and their wait is deferred).  The second workgroup of a CU starts half an item late
-// (flags & 0x1000 off; a per-CU arrival counter decides which one is second), so the two
-// epilogues alternate.
-//
-// Tile 256 (n) x 128 (m) per workgroup, K in 32-deep steps; wave (wn, wm) owns 128 n x 64 m =
-// 8 x 4 accumulators of 16 x 16 -- the same per-wave tile and accumulator layout as gemm16, so
-// g16_epilogue is shared.  Per step and wave: 8 W + 4 X fragments (ds_read_b128, or two
-// ds_read_b64_tr_b16 for a k-major W) for the NEXT step while 32 MFMAs consume this step's;
-// 6 LDS-DMA pieces of 1 KB for the step three ahead.  Stages: W [256 rows][32 k] and X [128
-// rows][32 k] (64-byte rows, 16-byte chunk c of row r at c ^ P_SWZ[(r >> 2) & 3], P_SWZ =
-// {0, 2, 3, 1}: each 16-lane group of a fragment ds_read_b128 hits 16 distinct bank slots), or
-// for a k-major W four [32 k][64 n] blocks in gemm16's k-major layout; 3 stages = 72 KB.
-namespace {
-constexpr int P_BK = 32, P_WIMG = 256 * P_BK, P_XIMG = 128 * P_BK, P_STAGE = P_WIMG + P_XIMG;
-constexpr int P_LDS = 3 * P_STAGE * 2;  // 72 KB
-ORION_DEVICE int p_swz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }
-
-ORION_DEVICE G16Item p_decode(const GemmArgs& g, int w) {
-  // groups of GM 128-row m-tiles with the m-tile fastest (as g16_decode)
-  const int GM = (g.flags >> 8) & 0xFF ? (g.flags >> 8) & 0xFF : 8;
-  const int tiles_m = (g.M + 127) >> 7;
-  G16Item it;
-  const int grp_sz = GM * g.tiles_n, gidx = w / grp_sz, first_m = gidx * GM;
-  const int gm = min(tiles_m - first_m, GM), in = w - gidx * grp_sz;
-  it.m0 = (first_m + in % gm) * 128;
-  it.n0 = (in / gm) * 256;
-  it.kc = 0;
-  it.k0 = 0;
-  it.kr = g.K;
-  it.nk = g.K / P_BK;
-  it.rows_m = min(g.M - it.m0, 128);
-  it.rows_n = min(g.N - it.n0, 256);
-  return it;
-}
-
-// store instructions every wave issues in g16_epilogue<EPI> unconditionally (a lower bound:
-// the deferred DMA waits after an epilogue may leave that many younger operations in flight)
-template <int EPI>
-constexpr int p_epi_stores() {
-  return (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) ? 32 : 16;
-}
-}  // namespace
-
-template <bool WKM, int EPI>
-__global__ __launch_bounds__(256, 2) void gemmp_kernel(GemmArgs g, unsigned* cu_ctr) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wv >> 1, wm = wv & 1;
-  const int q = lane >> 4, i16 = lane & 15;
-
-  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, lcl = bid >> 3;
-  const int tiles_m = (g.M + 127) >> 7, work = tiles_m * g.tiles_n;
-  const int wq = work >> 3, wr = work & 7;
-  const int r0 = xcd < wr ? xcd * (wq + 1) : wr * (wq + 1) + (xcd - wr) * wq;
-  const int rlen = wq + (xcd < wr ? 1 : 0);
-  const int stride = (nwg >> 3) + (xcd < (nwg & 7) ? 1 : 0);
-  const int nitems = lcl < rlen ? (rlen - lcl + stride - 1) / stride : 0;
-  if (nitems == 0) return;
-  auto item_id = [&](int j) { return r0 + lcl + j * stride; };
-  const int nk = g.K / P_BK;  // steps per item
-
-  // LDS-DMA: this wave's pieces of a stage -- W pieces 4 wv .. 4 wv + 3 (NT: 16 rows each;
-  // k-major: block wv, 8 k rows each), X pieces 2 wv, 2 wv + 1 (16 rows each)
-  const int lr4 = lane >> 2, c4 = lane & 3;  // NT piece: row, 16-byte chunk of the lane
-  unsigned wvo[4], xvo[2];
-  int wld[4], xld[2];
-  __amdgpu_buffer_rsrc_t rx, rw;
-  auto setup = [&](const G16Item& it) {
-    rx = make_rsrc(g.X + (long)it.m0 * g.ldx, (unsigned)(((long)(it.rows_m - 1) * g.ldx + g.K) * 2));
-    if constexpr (WKM)
-      rw = make_rsrc(g.W + it.n0, (unsigned)(((long)(g.K - 1) * g.ldw + it.rows_n) * 2));
-    else
-      rw = make_rsrc(g.W + (long)it.n0 * g.ldw, (unsigned)(((long)(it.rows_n - 1) * g.ldw + g.K) * 2));
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int row = 16 * (2 * wv + e) + lr4;  // 0..127
-      const int ch = c4 ^ p_swz(row);
-      xvo[e] = (unsigned)(((long)min(row, it.rows_m - 1) * g.ldx + 8 * ch) * 2);
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if constexpr (WKM) {  // block wv (64 n), k rows 8 e + lane / 8, 16-byte slot lane % 8
-        const int k = 8 * e + (lane >> 3), slot = lane & 7;
-        const int col = 64 * wv + 8 * (slot ^ (km_swz(k) << 1));
-        wvo[e] = (unsigned)(((long)k * g.ldw + min(col, it.rows_n - 8)) * 2);
-      } else {
-        const int row = 16 * (4 * wv + e) + lr4;  // 0..255
-        const int ch = c4 ^ p_swz(row);
-        wvo[e] = (unsigned)(((long)min(row, it.rows_n - 1) * g.ldw + 8 * ch) * 2);
-      }
-    }
-  };
-#pragma unroll
-  for (int e = 0; e < 4; ++e) wld[e] = WKM ? (wv * 64 * P_BK + e * 512) : (16 * (4 * wv + e)) * P_BK;
-#pragma unroll
-  for (int e = 0; e < 2; ++e) xld[e] = P_WIMG + (16 * (2 * wv + e)) * P_BK;
-
-  // the DMA stream: item index / step of the stage being issued, LDS stage counter
-  int ji = 0, ti = 0, si = 0;
-  G16Item cur_in = p_decode(g, item_id(0));
-  setup(cur_in);
-  const unsigned kstep_x = P_BK * 2, kstep_w = WKM ? (unsigned)(P_BK * g.ldw * 2) : P_BK * 2;
-  auto issue = [&]() {
-    bf16_t* base = smem + (si % 3) * P_STAGE;
-    const unsigned kx = (unsigned)ti * kstep_x, kw = (unsigned)ti * kstep_w;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) blds16(rw, wvo[e], kw, base + wld[e]);
-#pragma unroll
-    for (int e = 0; e < 2; ++e) blds16(rx, xvo[e], kx, base + xld[e]);
-    ++si;
-    if (ti + 1 < nk) {
-      ++ti;
-    } else if (ji + 1 < nitems) {
-      ++ji;
-      ti = 0;
-      cur_in = p_decode(g, item_id(ji));
-      setup(cur_in);
-    }
-    // past the last stage the stream re-loads it into a buffer nobody reads (same counts)
-  };
-
-  // fragment read offsets (bytes within a stage)
-  const unsigned lds0 = lds_addr(smem, 0);
-  const int frow = i16;  // row within a 16-row fragment block
-  const unsigned nto = (unsigned)(frow * 64 + ((q ^ p_swz(frow)) << 4));
-  int kmo[4];
-  {
-    const int row0 = 8 * q + (i16 >> 2), h = km_swz(row0);
-#pragma unroll
-    for (int b = 0; b < 4; ++b) kmo[b] = row0 * 128 + ((b ^ h) << 5) + 8 * (i16 & 3);
-  }
-  // W fragments as two 8-byte halves (k-major: two ds_read_b64_tr_b16; NT: one ds_read_b128
-  // split): an asm read's destination is "written" at the statement for the compiler, so a
-  // concatenation before the wait could copy registers the LDS has not filled yet -- the
-  // halves stay separate until the step's lgkmcnt(0) names them
-  auto read_frags = [&](bf16x4 (&Wl)[8], bf16x4 (&Wh)[8], bf16x8 (&W8)[8], bf16x8 (&Xf)[4], int s) {
-    const unsigned st0 = lds0 + (unsigned)((s % 3) * P_STAGE * 2);
-    if constexpr (WKM) {
-      const unsigned wb = st0 + (unsigned)(2 * wn) * 4096u;
-#pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        const unsigned ad = wb + (unsigned)((a >> 2) * 4096) + (unsigned)kmo[a & 3];
-        Wl[a] = rd_tr<0>(ad);
-        Wh[a] = rd_tr<512>(ad);
-      }
-    } else {
-      const unsigned wa = st0 + (unsigned)(wn * 128 * 64) + nto;
-      W8[0] = rd_b128<0>(wa);
-      W8[1] = rd_b128<1024>(wa);
-      W8[2] = rd_b128<2048>(wa);
-      W8[3] = rd_b128<3072>(wa);
-      W8[4] = rd_b128<4096>(wa);
-      W8[5] = rd_b128<5120>(wa);
-      W8[6] = rd_b128<6144>(wa);
-      W8[7] = rd_b128<7168>(wa);
-    }
-    const unsigned xa = st0 + (unsigned)(P_WIMG * 2 + wm * 64 * 64) + nto;
-    Xf[0] = rd_b128<0>(xa);
-    Xf[1] = rd_b128<1024>(xa);
-    Xf[2] = rd_b128<2048>(xa);
-    Xf[3] = rd_b128<3072>(xa);
-  };
-
-  f32x4 acc[8][4];
-  bf16x4 WAl[8], WAh[8], WBl[8], WBh[8];  // k-major W (two halves per fragment)
-  bf16x8 WA8[8], WB8[8];                  // NT W
-  bf16x8 XA[4], XB[4];
-
-  // optional start offset of the CU's second workgroup (half an item of sleep)
-  if (g.flags & 0x1000) {
-    unsigned key = 0;
-    if (tid == 0) {
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-      const unsigned xc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-      key = ((xc & 7) << 8) | ((hw >> 8) & 0xFF);  // cu, sh, se
-      const unsigned order = atomicAdd(&cu_ctr[key], 1u);
-      reinterpret_cast<unsigned*>(smem)[P_LDS / 4 - 1] = order;
-    }
-    __syncthreads();
-    const unsigned order = reinterpret_cast<unsigned*>(smem)[P_LDS / 4 - 1];
-    __syncthreads();
-    if (order & 1) {
-      for (int i = 0; i < nk / 2; ++i) __builtin_amdgcn_s_sleep(16);  // ~1 k cycles per step
-    }
-  }
-
-  // prologue: stages 0, 1, 2; stage 0 landed -> its fragments
-  issue();
-  issue();
-  issue();
-  wait_vm_exact<12>();
-  g_barrier();
-  read_frags(WAl, WAh, WA8, XA, 0);
-
-  constexpr int SD = p_epi_stores<EPI>();
-  int since_epi = 2;  // steps since the last epilogue (deferred waits for 2 steps)
-  int s = 0;
-  // the epilogues that stream operands (GELU' / SwiGLU') need the registers of the next item's
-  // prefetched fragments: they re-read them after the epilogue instead
-  constexpr bool XPF = !(EPI == EPI_GELU_BWD || EPI == EPI_SWIGLU_BWD);
-  auto step = [&](bf16x4 (&Wcl)[8], bf16x4 (&Wch)[8], bf16x8 (&Wc8)[8], bf16x8 (&Xc)[4], bf16x4 (&Wnl)[8],
-                  bf16x4 (&Wnh)[8], bf16x8 (&Wn8)[8], bf16x8 (&Xn)[4], bool rd) {
-    // this step's fragments landed (issued last step); stage s + 1 landed (issued two steps ago)
-    if constexpr (WKM)
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(Wcl[0]), "+v"(Wcl[1]), "+v"(Wcl[2]), "+v"(Wcl[3]), "+v"(Wcl[4]), "+v"(Wcl[5]),
-                     "+v"(Wcl[6]), "+v"(Wcl[7]), "+v"(Wch[0]), "+v"(Wch[1]), "+v"(Wch[2]), "+v"(Wch[3]),
-                     "+v"(Wch[4]), "+v"(Wch[5]), "+v"(Wch[6]), "+v"(Wch[7]), "+v"(Xc[0]), "+v"(Xc[1]),
-                     "+v"(Xc[2]), "+v"(Xc[3]));
-    else
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(Wc8[0]), "+v"(Wc8[1]), "+v"(Wc8[2]), "+v"(Wc8[3]), "+v"(Wc8[4]), "+v"(Wc8[5]),
-                     "+v"(Wc8[6]), "+v"(Wc8[7]), "+v"(Xc[0]), "+v"(Xc[1]), "+v"(Xc[2]), "+v"(Xc[3]));
-    if (since_epi < 2) wait_vm_exact<6 + SD>();
-    else wait_vm_exact<6>();
-    g_barrier();
-    issue();                       // stage s + 3 into the buffer of stage s (read last step)
-    if (rd) read_frags(Wnl, Wnh, Wn8, Xn, s + 1);  // next step's fragments
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      const bf16x8 wf = WKM ? cat8(Wcl[a], Wch[a]) : Wc8[a];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = mfma16(wf, Xc[b], acc[a][b]);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    ++s;
-    ++since_epi;
-  };
-
-  for (int j = 0; j < nitems; ++j) {
-    const G16Item it = p_decode(g, item_id(j));
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = zero4();
-    // nk is even (K % 64 == 0): the two register sets alternate in pairs of steps
-    for (int t = 0; t < nk; t += 2) {
-      step(WAl, WAh, WA8, XA, WBl, WBh, WB8, XB, true);
-      step(WBl, WBh, WB8, XB, WAl, WAh, WA8, XA, XPF || t + 2 < nk);
-    }
-    g16_epilogue<EPI>(g, acc, it, wm, wn, q, i16);
-    since_epi = 0;
-    if constexpr (!XPF) {
-      // the next item's first fragments (stage s landed: waited at the top of the last step)
-      read_frags(WAl, WAh, WA8, XA, s);
-    }
-  }
-  wait_vm_exact<0>();  // the stream's last (dummy) LDS-DMA lands before the LDS is freed
-}
-
 template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
 static int gemm16_launch(const GemmArgs& a, hipStream_t st) {
   if constexpr (!STAMPS && EPI == EPI_STORE) {
@@ -1034,51 +771,6 @@ int gemm16(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
     case EPI_SWIGLU_BWD * 2 + 1: return gemm16_launch<false, true, EPI_SWIGLU_BWD>(a, st);
     case EPI_EXP * 2 + 0: return gemm16_launch<false, false, EPI_EXP>(a, st);
     case EPI_ROWSCALE * 2 + 1: return gemm16_launch<false, true, EPI_ROWSCALE>(a, st);
-    default: return -4;
-  }
-}
-
-// gemmp launch: grid 2 x 256 workgroups (two per CU by the 72 KB LDS plan and 256 VGPRs),
-// fewer when there is less work; cu_ctr: the per-CU arrival counters of the start offset
-// (zeroed per call when flags & 0x1000).
-static unsigned* p_counters(hipStream_t st) {
-  static unsigned* ctr = nullptr;
-  if (!ctr && hipMalloc(&ctr, 2048 * sizeof(unsigned)) != hipSuccess) ctr = nullptr;
-  if (ctr) (void)hipMemsetAsync(ctr, 0, 2048 * sizeof(unsigned), st);
-  return ctr;
-}
-
-template <bool WKM, int EPI>
-static int gemmp_launch(const GemmArgs& a, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemmp_kernel<WKM, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            P_LDS) != hipSuccess)
-      return -5;
-    attr = true;
-  }
-  const long work = (long)((a.M + 127) / 128) * a.tiles_n;
-  if (work <= 0 || work > 0x7FFFFFFFL || a.K % 64) return -1;
-  unsigned* ctr = (a.flags & 0x1000) ? p_counters(st) : nullptr;
-  if ((a.flags & 0x1000) && !ctr) return -6;
-  const unsigned grid = work < 512 ? (unsigned)work : 512u;
-  gemmp_kernel<WKM, EPI><<<grid, 256, P_LDS, st>>>(a, ctr);
-  return (int)hipGetLastError();
-}
-
-int gemmp(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
-  GemmArgs a = a0;
-  a.kchunk = a.K;
-  a.ksplit = 1;
-  switch (epi * 2 + (wkm ? 1 : 0)) {
-    case EPI_STORE * 2 + 0: return gemmp_launch<false, EPI_STORE>(a, st);
-    case EPI_STORE * 2 + 1: return gemmp_launch<true, EPI_STORE>(a, st);
-    case EPI_BIAS * 2 + 0: return gemmp_launch<false, EPI_BIAS>(a, st);
-    case EPI_BIAS_GELU * 2 + 0: return gemmp_launch<false, EPI_BIAS_GELU>(a, st);
-    case EPI_GELU_BWD * 2 + 1: return gemmp_launch<true, EPI_GELU_BWD>(a, st);
-    case EPI_SWIGLU_BWD * 2 + 1: return gemmp_launch<true, EPI_SWIGLU_BWD>(a, st);
-    case EPI_EXP * 2 + 0: return gemmp_launch<false, EPI_EXP>(a, st);
-    case EPI_ROWSCALE * 2 + 1: return gemmp_launch<true, EPI_ROWSCALE>(a, st);
     default: return -4;
   }
 }

@@ -53,12 +53,6 @@ ORION_DEVICE bf16x8 rd_b128(unsigned a) {
   return r;
 }
 
-ORION_DEVICE bf16x8 rd_b128_dyn(unsigned a) {
-  bf16x8 r;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-
 template <int OFF>
 ORION_DEVICE bf16x4 rd_tr(unsigned a) {
   bf16x4 r;
@@ -90,7 +84,5 @@ ORION_DEVICE void g_wait_lds(bf16x8 (&a)[4][2]) {
 bool gemm16_ok(const GemmArgs& a, int wkm);
 int gemm16(const GemmArgs& a, int wkm, int epi, hipStream_t st);
 int gemm16_wgrad(const GemmArgs& a, hipStream_t st);
-// two workgroups per CU (short-K GEMMs with epilogues): same arguments as gemm16
-int gemmp(const GemmArgs& a, int wkm, int epi, hipStream_t st);
 
 }  // namespace orion

@@ -4,9 +4,8 @@ csrc/gemm16.hip (with its fused epilogues) vs hipBLASLt through PyTorch (committ
 table loaded) plus the separate HIP epilogue kernels it needs.  Interleaved rounds in one
 process, median per variant; one JSON line per shape.
 
-usage: python scripts/bench_gemm.py [--M 65536] [--iters 20] [--check] [--cfgs p,s,w,o]
-(cfgs: p gemm16 persistent, s one workgroup per item, w gemmp two workgroups per CU, o gemmp
-with the second workgroup of a CU started half an item late)
+usage: python scripts/bench_gemm.py [--M 65536] [--iters 20] [--check] [--cfgs p,s]
+(cfgs: p gemm16 persistent, s one workgroup per item)
 """
 import argparse
 import json
@@ -114,7 +113,7 @@ def main():
                 blas = lambda: x @ w
         def with_cfg(c, f):
             def run():
-                ops.gemm_diag({"s": 64, "w": 0x2000, "o": 0x3000}.get(c, 0))
+                ops.gemm_diag({"s": 64}.get(c, 0))
                 return f()
             return run
         fns = {f"hip{c}": with_cfg(c, hip) for c in cfgs}

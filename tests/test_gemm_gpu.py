@@ -36,13 +36,12 @@ SHAPES = [(256, 256, 64), (300, 264, 128), (1000, 768, 768), (513, 1000, 192), (
           (65536, 768, 768)]
 
 
-@pytest.fixture(params=["persistent", "per_item", "pair", "pair_offset"])
+@pytest.fixture(params=["persistent", "per_item"])
 def gemm_cfg(request):
-    """gemm16's persistent walk (one workgroup per CU, continuous DMA stream across items),
-    the one-workgroup-per-item launch (diagnostic flag 64), and the two-workgroups-per-CU
-    kernel gemmp (flag 0x2000; 0x1000: the CU's second workgroup starts half an item late)."""
+    """gemm16's persistent walk (one workgroup per CU, continuous DMA stream across items)
+    and the one-workgroup-per-item launch (diagnostic flag 64)."""
     C = _C()
-    old = C.gemm_diag({"per_item": 64, "pair": 0x2000, "pair_offset": 0x3000}.get(request.param, 0))
+    old = C.gemm_diag(64 if request.param == "per_item" else 0)
     yield request.param
     C.gemm_diag(old)
 
