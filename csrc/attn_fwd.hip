@@ -343,6 +343,219 @@ __global__ __launch_bounds__(256, 2) void attn_fwd3_kernel(AttnParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// attn_fwd4 (round 5, D = 64): four waves per SIMD.  The round-3/4 forward holds 255 VGPRs
+// (two 32-row query blocks per wave, K / V staged through registers) and so runs at two waves
+// per SIMD, where its per-tile chain (S MFMAs -> row max -> exp -> pack -> PV MFMAs) is
+// latency-bound: stamps put half a tile in the softmax phase and a quarter at the barrier
+// (docs/PERFORMANCE.md, "Attention").  Here one 32-row block per wave, K / V tiles arrive by
+// LDS-DMA (no staging registers), the LDS fragment reads are inline asm with hand-counted
+// waits (the compiler's wait-count pass would drain the DMA ring before its own LDS reads),
+// and the register diet (Q 16, O 32, S 32 / P 16, one block of K or V fragments 16) keeps the
+// kernel under 128 VGPRs: four workgroups of 4 waves per CU (32 KB of LDS each), so every
+// SIMD interleaves four waves' chains.  Same algorithm and numerics as attn_fwd3: swapped
+// S^T = K Q^T with the query on the lane, online softmax in base 2 with the deferred rescale,
+// P from the accumulators into O^T += V^T P^T.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 4) void attn_fwd4_kernel(AttnParams p) {
+  constexpr int D = 64, BM = 128, BN = 64, TILE = BN * D;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int BH = p.B * p.Hq;
+  const int nqt = (p.T + BM - 1) / BM;
+  const int bh = blockIdx.x % BH;
+  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) tiles launch first
+  const int b = bh / p.Hq, hq = bh % p.Hq, hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qt * BM, qw0 = q0 + wv * 32;
+  const int off = p.Tk - p.T;  // causal: key <= query + off
+  const float c = p.scale_log2;
+
+  const bf16_t* Qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
+
+  bf16x8 qf[D / 16];
+  {
+    const int qr = min(qw0 + l32, p.T - 1);
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks)
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * p.q_st + ks * 16 + 8 * h32);
+  }
+  const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
+  const int ntiles = (kend + BN - 1) / BN;
+
+  // LDS-DMA: a tile's K (and V) image is 8 pieces of 8 rows x 128 bytes; wave wv issues
+  // pieces 2 wv, 2 wv + 1 of each.  Lane: row 8 pc + lane / 8, physical chunk lane % 8, read
+  // from the logical chunk (lane % 8) ^ swz<64>(row) (loff<64>'s XOR, an involution).  Full
+  // tiles advance by the scalar offset; a last partial tile clamps its rows to the last key.
+  const unsigned kst_b = (unsigned)p.k_st * 2, vst_b = (unsigned)p.v_st * 2;
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc(Kb, (unsigned)((long)(p.Tk - 1) * p.k_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(Vb, (unsigned)((long)(p.Tk - 1) * p.v_st + D) * 2);
+  const int prow0 = 16 * wv + (lane >> 3);  // piece e adds 8 rows
+  auto dma = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    bf16_t* Ks = smem + buf * 2 * TILE;
+    const int k0 = t * BN;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = prow0 + 8 * e;
+      const unsigned ch16 = 16u * (unsigned)((lane & 7) ^ swz<D>(row));
+      if (k0 + BN <= p.Tk) {
+        blds16(rk, (unsigned)row * kst_b + ch16, (unsigned)k0 * kst_b, Ks + (2 * wv + e) * 512);
+        blds16(rv, (unsigned)row * vst_b + ch16, (unsigned)k0 * vst_b, Ks + TILE + (2 * wv + e) * 512);
+      } else {
+        const unsigned key = (unsigned)min(k0 + row, p.Tk - 1);
+        blds16(rk, key * kst_b + ch16, 0, Ks + (2 * wv + e) * 512);
+        blds16(rv, key * vst_b + ch16, 0, Ks + TILE + (2 * wv + e) * 512);
+      }
+    }
+  };
+  // per-lane LDS byte bases: K rows l32 (d chunk 2 ks + h32: four bases, the key block by an
+  // immediate); V transposed reads of key rows kk 16 + 4 h32 + (iq >> 2) (+ 8: second half),
+  // columns db 32 + 16 (gq & 1) + 4 (iq & 3) -- the swizzle does not depend on kk, so one base
+  // per (db, half) and kk by an immediate
+  const unsigned lds0 = lds_addr(smem, 0);
+  unsigned kad[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) kad[ks] = lds0 + 2u * (unsigned)loff<D>(l32, ks * 16 + 8 * h32);
+  const int gq = lane >> 4, iq = lane & 15;
+  unsigned vad[2][2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+      vad[db][hf] = lds0 + 2u * (unsigned)(TILE + loff<D>(4 * h32 + (iq >> 2) + 8 * hf, db * 32 + 16 * (gq & 1) + 4 * (iq & 3)));
+
+  f32x16 oacc[2];
+  oacc[0] = zero16();
+  oacc[1] = zero16();
+  float m = -1e30f, lsum = 0.f;
+
+  auto tile = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    constexpr unsigned BOFF = buf * 2 * TILE * 2;  // bytes
+    // tile t landed (this wave's pieces; the barrier: everyone's) and every wave is done with
+    // the other buffer (read in tile t - 1): tile t + 1 may overwrite it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < ntiles) dma(t + 1, std::integral_constant<int, buf ^ 1>{});
+    const int k0 = t * BN;
+    const bool active = !CAUSAL || (k0 <= qw0 + 31 + off);
+    if (!active) return;
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 kf[D / 16];
+      if (kb == 0) {
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) kf[ks] = b128_read_at<BOFF>(kad[ks]);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) kf[ks] = b128_read_at<BOFF + 32 * D * 2>(kad[ks]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]));
+      s[kb] = zero16();
+      mfma_prio(true);
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) s[kb] = mfma32(kf[ks], qf[ks], s[kb]);
+      mfma_prio(false);
+    }
+    const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw0 + off)) || (k0 + BN > p.Tk);
+    if (need_mask) {
+      const int vis = CAUSAL ? min(qw0 + l32 + off, p.Tk - 1) : p.Tk - 1;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int lim = vis - (k0 + kb * 32 + 4 * h32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[kb][r];
+      }
+    }
+    float mx4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x16& a = s[j >> 1];
+      const int r0 = (j & 1) * 8;
+      float x = max3f(a[r0], a[r0 + 1], a[r0 + 2]);
+      x = max3f(x, a[r0 + 3], a[r0 + 4]);
+      x = max3f(x, a[r0 + 5], a[r0 + 6]);
+      mx4[j] = max3f(x, a[r0 + 7], m);
+    }
+    float mx = max3f(mx4[0], mx4[1], max3f(mx4[2], mx4[3], m));
+    mx = half_max(mx);
+    float alpha = 1.f;
+    if (__any((mx - m) * c > 8.f)) {
+      alpha = __builtin_amdgcn_exp2f((m - mx) * c);
+      m = mx;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+    }
+    const float mc = m * c;
+    float ps4[4] = {0.f, 0.f, 0.f, 0.f};
+    bf16x8 pf[4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * s2 + j], c, -mc));
+          ps4[j & 3] = addf(ps4[j & 3], e);
+          pf[kb * 2 + s2][j] = f2bf(e);
+        }
+    lsum = fmaf(lsum, alpha, addf(addf(ps4[0], ps4[1]), addf(ps4[2], ps4[3])));
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      // V^T fragments: two transposed 4-row reads each, kept as halves until their wait
+      bf16x4 vlo[4], vhi[4];
+      vlo[0] = tr_read_at<BOFF + 0 * 16 * D * 2>(vad[db][0]);
+      vhi[0] = tr_read_at<BOFF + 0 * 16 * D * 2>(vad[db][1]);
+      vlo[1] = tr_read_at<BOFF + 1 * 16 * D * 2>(vad[db][0]);
+      vhi[1] = tr_read_at<BOFF + 1 * 16 * D * 2>(vad[db][1]);
+      vlo[2] = tr_read_at<BOFF + 2 * 16 * D * 2>(vad[db][0]);
+      vhi[2] = tr_read_at<BOFF + 2 * 16 * D * 2>(vad[db][1]);
+      vlo[3] = tr_read_at<BOFF + 3 * 16 * D * 2>(vad[db][0]);
+      vhi[3] = tr_read_at<BOFF + 3 * 16 * D * 2>(vad[db][1]);
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(vlo[0]), "+v"(vlo[1]), "+v"(vlo[2]), "+v"(vlo[3]), "+v"(vhi[0]), "+v"(vhi[1]),
+                     "+v"(vhi[2]), "+v"(vhi[3]));
+      mfma_prio(true);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) oacc[db] = mfma32(cat8(vlo[kk], vhi[kk]), pf[kk], oacc[db]);
+      mfma_prio(false);
+    }
+  };
+
+  dma(0, std::integral_constant<int, 0>{});
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the workgroup ends
+
+  const int myq = qw0 + l32;
+  const float lt = half_sum(lsum);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (myq < p.T) {
+    bf16_t* Ob = p.o + b * p.o_sb + hq * p.o_sh + (long)myq * p.o_st;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(oacc[db][4 * g4 + j] * inv);
+        *reinterpret_cast<bf16x4*>(Ob + db * 32 + 8 * g4 + 4 * h32) = v4;
+      }
+    if (h32 == 0) p.lse[((long)b * p.Hq + hq) * p.T + myq] = m * c + __log2f(lt);
+  }
+}
+
 }  // namespace orion
 
 using namespace orion;
@@ -359,6 +572,27 @@ static void fwd3_attr() {
   }
 }
 
+template <bool CAUSAL>
+static void fwd4_launch(const AttnParams& p, hipStream_t st) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd4_kernel<CAUSAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * 2 * 64 * 64 * 2);
+    done = true;
+  }
+  attn_fwd4_kernel<CAUSAL><<<((p.T + 127) / 128) * p.B * p.Hq, 256, 2 * 2 * 64 * 64 * 2, st>>>(p);
+}
+
+// ORION_ATTN_FWD=v3: the D = 64 forward of rounds 3-4 (A/B); default attn_fwd4
+static bool fwd_v3() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORION_ATTN_FWD");
+    v = (e && e[0] == 'v' && e[1] == '3') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 template <int D, bool CAUSAL>
 static void fwd3_launch(const AttnParams& p, int qb64, size_t lds, hipStream_t st) {
   if constexpr (D == 64 && CAUSAL) {
@@ -368,6 +602,15 @@ static void fwd3_launch(const AttnParams& p, int qb64, size_t lds, hipStream_t s
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 64 * D * 2);
       attn_fwd3_kernel<64, true, 2, true><<<((p.T + 255) / 256) * p.B * p.Hq, 256, lds, st>>>(p);
       return;
+    }
+  }
+  if constexpr (D == 64) {
+    static const bool diag = getenv("ORION_ATTN_FWD_DIAG") && getenv("ORION_ATTN_FWD_DIAG")[0] == '1';
+    if constexpr (CAUSAL) {  // the non-causal form runs out of registers at 4 waves: fwd3
+      if (!diag && !fwd_v3()) {
+        fwd4_launch<CAUSAL>(p, st);
+        return;
+      }
     }
   }
   if constexpr (D == 64) {

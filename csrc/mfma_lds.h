@@ -105,6 +105,20 @@ ORION_DEVICE bf16x4 tr_read(const bf16_t* lds, int elem) {
   return r;
 }
 
+// the same reads at a byte address + an immediate offset (loop-invariant per-lane bases)
+template <int OFF>
+ORION_DEVICE bf16x4 tr_read_at(unsigned a) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+template <int OFF>
+ORION_DEVICE bf16x8 b128_read_at(unsigned a) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+
 ORION_DEVICE bf16x8 b128_read(const bf16_t* lds, int elem) {
   bf16x8 r;
   asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(lds_addr(lds, elem)));

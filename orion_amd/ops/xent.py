@@ -68,7 +68,13 @@ _CREF = {}
 
 def _cref(dev):
     """The running exp reference of the LM-head forward on ``dev`` (a device scalar the fold
-    kernel updates: the largest row log-sum-exp of the previous call)."""
+    kernel updates: the largest row log-sum-exp of the previous call).  Deterministic mode
+    (ops/determinism.py) uses a fresh 0 every call instead: the bf16 rounding of exp(logit -
+    ref) depends on the reference, so a carried-over one would make two identical runs in one
+    process differ in the last bits (rows it does not suit take the exact fixup path)."""
+    from .determinism import deterministic
+    if deterministic():
+        return torch.zeros(1, dtype=torch.float32, device=dev)
     t = _CREF.get(dev)
     if t is None:
         t = _CREF[dev] = torch.zeros(1, dtype=torch.float32, device=dev)

@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--square", type=int, default=0, help="also time an NT GEMM of this cube size")
     ap.add_argument("--only", default="", help="comma list of shape names to run")
     ap.add_argument("--llama", action="store_true", help="Llama-2-7B shapes (M = 16,384 tokens) instead")
+    ap.add_argument("--step-data", action="store_true",
+                    help="operands distributed like the training step's (activations N(0, 1), weights "
+                         "N(0, 0.02^2)) instead of N(0, 0.5^2) for both: the chip's clock depends on the data")
     a = ap.parse_args()
     from orion_amd.ops._ext import C, load_ext
     from orion_amd.tuning import use_tuned_gemms
@@ -84,6 +87,9 @@ def main():
             M = a.M
         x = rnd(M, K)
         w = rnd(N, K) if kind == "fwd" else rnd(K, N)
+        if a.step_data:
+            x = (x.float() * 2.0).bfloat16()
+            w = (w.float() * 0.04).bfloat16()
         b = rnd(N) if epi in (1, 2, 5) else None
         pre = rnd(M, N) if epi in (3, 5) else None
         if epi == 6:  # LM head: exp epilogue + fold (csrc/lmhead.hip) vs hipBLASLt logits
