@@ -611,7 +611,7 @@ std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor,
     bp = bc.data_ptr();
   }
   if (epi == 2) out2 = at::empty(sizes, x.options());
-  if (epi == 0 && pre.has_value() && pre->defined() && pre->nbytes() >= 8 * 8 * 1024)
+  if (epi <= 2 && pre.has_value() && pre->defined() && pre->nbytes() >= 8 * 8 * 1024)
     pp = pre->data_ptr();  // diagnostic: the gemm_diag(4) slot-stamp buffer (scripts/gemm16_stamps.py)
   if (epi == 3) {
     TORCH_CHECK(pre.has_value() && pre->defined(), "gemm: GELU backward needs the pre-activation");

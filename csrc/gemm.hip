@@ -77,7 +77,7 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   GemmArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)out, ldo,
              (const bf16_t*)bias, (bf16_t*)out2, ldo2, (const bf16_t*)pre, ldp,
              M, N, K, (N + 255) / 256, gemm_diag()};
-  if ((a.flags & 4) && epi == EPI_STORE) a.slabs = (float*)pre;  // slot stamps (diagnostic)
+  if ((a.flags & 4) && epi <= EPI_BIAS_GELU) a.slabs = (float*)pre;  // slot stamps (diagnostic)
   if (!gemm16_ok(a, wkm)) return -1;
   const int rows = (M + 63) / 64;
   if (db) a.colsum = part;

@@ -104,11 +104,53 @@ ORION_DEVICE G16Item g16_decode(const GemmArgs& g, int w) {
 #ifndef G16_ST_AUX
 #define G16_ST_AUX 2
 #endif
+#ifndef G16_ST2_AUX
+#define G16_ST2_AUX G16_ST_AUX  // the second output (GELU activation / SwiGLU dup)
+#endif
+// diagnostic: G16_DIAG_GELU=0 replaces GELU / GELU' by the identity (same loads and stores)
+// to price the epilogue's transcendental arithmetic
+#ifndef G16_DIAG_GELU
+#define G16_DIAG_GELU 1
+#endif
+// diagnostics of the epilogue's cost (round 5, profiles/ab/gemm16_epilogue_pricing_r05.log):
+// G16_DIAG_ST2=0 issues no second-output stores (GELU activation / SwiGLU dup);
+// G16_DIAG_ST2_SMALL=1 folds the second output into its first 256 KB (L2-resident);
+// G16_DEFER=1: the first phase after an epilogue waits only for the pieces issued before that
+// epilogue's stores (vmcnt(4 + stores)).  Measured and removed: odd workgroups starting half an
+// item late (stagger), the bias loads moved into the last k-tile (spills).
+#ifndef G16_DIAG_ST2
+#define G16_DIAG_ST2 1
+#endif
+#ifndef G16_DIAG_ST2_SMALL
+#define G16_DIAG_ST2_SMALL 0
+#endif
+#ifndef G16_DEFER
+#define G16_DEFER 0
+#endif
+// G16_EPI_SYNC: both groups' epilogues between the same pair of barriers (see the item loop)
+#ifndef G16_EPI_SYNC
+#define G16_EPI_SYNC 1
+#endif
 
 // The epilogue of one work item (registers only, no LDS).
 template <int EPI>
+ORION_DEVICE constexpr bool g16_has_bias() { return EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_GELU_BWD; }
+
+// the bias of the wave's four column groups (8 consecutive n per lane after the swap)
+template <int EPI>
+ORION_DEVICE void g16_load_bias(const GemmArgs& g, const G16Item& it, int grp, int q, u32x4 (&bias4)[4]) {
+  const int nw = it.n0 + grp * 128;
+#pragma unroll
+  for (int ap = 0; ap < 4; ++ap) {
+    const int nb = nw + 16 * (2 * ap + (q & 1)) + 8 * (q >> 1), nc = nb < g.N ? nb : 0;
+    if (EPI != EPI_GELU_BWD || g.bias) bias4[ap] = *reinterpret_cast<const u32x4*>(g.bias + nc);
+    else bias4[ap] = u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+template <int EPI>
 ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16Item& it, int wm, int grp,
-                               int q, int i16) {
+                               int q, int i16, u32x4 (&bias4)[4]) {
   const int m0 = it.m0, kc = it.kc, rows_m = it.rows_m;
   const int mw = m0 + wm * 64;           // this wave's 64-row block
   const int nw = it.n0 + grp * 128;      // this wave's 128 columns
@@ -160,15 +202,7 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
   // vmcnt(0), which on CDNA4 also waits for the stores -- the GELU' epilogue ran as 17
   // serial HBM round trips per wave.  The fragment registers of the main loop are dead here.
   auto ncol = [&](int ap) { return nw + 16 * (2 * ap + (q & 1)) + 8 * (q >> 1); };
-  [[maybe_unused]] u32x4 bias4[4];
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_GELU_BWD) {
-#pragma unroll
-    for (int ap = 0; ap < 4; ++ap) {
-      const int nb = ncol(ap), nc = nb < g.N ? nb : 0;
-      if (EPI != EPI_GELU_BWD || g.bias) bias4[ap] = *reinterpret_cast<const u32x4*>(g.bias + nc);
-      else bias4[ap] = u32x4{0u, 0u, 0u, 0u};
-    }
-  }
+  if constexpr (g16_has_bias<EPI>()) g16_load_bias<EPI>(g, it, grp, q, bias4);
   // GELU' / SwiGLU' operands (the pre-activation, or the gate and up halves of the packed
   // gate_up projection) stream in one column group (ap) ahead of their use: the loads of group
   // ap + 1 are issued before the stores of group ap, so waiting for them never waits for those
@@ -254,7 +288,7 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       }
       if constexpr (EPI == EPI_GELU_BWD) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] *= gelu_grad_x2(unpack2(p4[e]) + bias[e]);
+        for (int e = 0; e < 4; ++e) v[e] *= G16_DIAG_GELU ? gelu_grad_x2(unpack2(p4[e]) + bias[e]) : unpack2(p4[e]) + bias[e];
       }
       if constexpr (EPI == EPI_EXP) {
         // the target's logit (fp32, before the exp) for the loss; exp(acc - cref) and its row sum
@@ -296,7 +330,7 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if constexpr (EPI == EPI_BIAS_GELU) pk2[e] = pack2_bf16(gelu_x2(v[e]));
+          if constexpr (EPI == EPI_BIAS_GELU) pk2[e] = pack2_bf16(G16_DIAG_GELU ? gelu_x2(v[e]) : v[e] * v[e]);
           else pk2[e] = pack2_bf16(du[e]);
         }
       }
@@ -331,12 +365,16 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
           const unsigned o1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo + ncx) * 2) : 0xFFFFFFF0u;
           __builtin_amdgcn_raw_buffer_store_b128(n0, ro, o0, 0, AUX1);
           __builtin_amdgcn_raw_buffer_store_b128(n1, ro, o1, 0, AUX1);
-          if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
+          if constexpr ((EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) && G16_DIAG_ST2) {
             xchg(parkB[b], pk2, n0, n1);
-            const unsigned p0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
-            const unsigned p1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
-            __builtin_amdgcn_raw_buffer_store_b128(n0, ro2, p0, 0, G16_ST_AUX);
-            __builtin_amdgcn_raw_buffer_store_b128(n1, ro2, p1, 0, G16_ST_AUX);
+            unsigned p0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
+            unsigned p1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
+#if G16_DIAG_ST2_SMALL  // diagnostic: the second output folded into its first 256 KB (L2-resident)
+            p0 &= 0x3FFF0u;
+            p1 &= 0x3FFF0u;
+#endif
+            __builtin_amdgcn_raw_buffer_store_b128(n0, ro2, p0, 0, G16_ST2_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(n1, ro2, p1, 0, G16_ST2_AUX);
           }
         }
       } else {
@@ -345,7 +383,7 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
         __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, AUX1);
         if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
           const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
-          __builtin_amdgcn_raw_buffer_store_b128(pk2, ro2, off2, 0, G16_ST_AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(pk2, ro2, off2, 0, G16_ST2_AUX);
         }
       }
       if constexpr (CS) {
@@ -398,8 +436,8 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
   }
 }
 
-// STAMPS (diagnostic instantiation: ORION_GEMM_DIAG=4 with a stamp buffer, EPI_STORE only,
-// one item per workgroup): every wave of every workgroup records s_memtime at 16 points --
+// STAMPS (diagnostic instantiation: ORION_GEMM_DIAG=4 with a stamp buffer, EPI_STORE / BIAS /
+// BIAS_GELU, one item per workgroup or (flags & 128) the persistent walk): every wave of every workgroup records s_memtime at 16 points --
 // kernel start, prologue landed, the 6 slot boundaries of both phases of the middle k-tile
 // (READ start, reads+DMA issued, vmcnt retired, MMA slot entered, fragments landed, MFMAs
 // issued), main loop done, epilogue issued -- plus where it ran (HW_ID / XCC_ID) into g.slabs
@@ -411,7 +449,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wv >> 2, wm = wv & 3;
   const int q = lane >> 4, i16 = lane & 15;
-  [[maybe_unused]] unsigned long stp[20];
+  [[maybe_unused]] unsigned long stp[20] = {};
   if constexpr (STAMPS) stp[0] = __builtin_amdgcn_s_memtime();
 
   // this workgroup's items: the work ids of XCD group b % 8 are one contiguous range of the
@@ -426,6 +464,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   const int nitems = lcl < rlen ? (rlen - lcl + stride - 1) / stride : 0;
   if (nitems == 0) return;
   auto item_id = [&](int j) { return r0 + lcl + j * stride; };
+  auto decode = [&](int j) { return g16_decode(g, item_id(j)); };
 
   const unsigned xstep = XKM ? (unsigned)(G_BK * g.ldx * 2) : G_BK * 2;
   const unsigned wstep = WKM ? (unsigned)(G_BK * g.ldw * 2) : G_BK * 2;
@@ -507,7 +546,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   int jx = 0, tx = 0, sx = 0, jw = 0, tw = 0, sw = 0;
   int nkx, nkw;
   {
-    const G16Item it = g16_decode(g, item_id(0));
+    const G16Item it = decode(0);
     setup_x(it);
     setup_w(it);
     nkx = nkw = it.nk;
@@ -536,7 +575,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
     } else if (jx + 1 < nitems) {
       ++jx;
       tx = 0;
-      const G16Item it = g16_decode(g, item_id(jx));
+      const G16Item it = decode(jx);
       setup_x(it);
       nkx = it.nk;
     }
@@ -548,7 +587,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
     } else if (jw + 1 < nitems) {
       ++jw;
       tw = 0;
-      const G16Item it = g16_decode(g, item_id(jw));
+      const G16Item it = decode(jw);
       setup_w(it);
       nkw = it.nk;
     }
@@ -616,16 +655,26 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
-  int tsel = -1;
+  // stamped item: the only one (one workgroup per item) or, on the persistent walk (flags &
+  // 128), the middle one; its successor's first k-tile stamps its wait / barrier exits
+  [[maybe_unused]] const bool spers = STAMPS && (g.flags & 128);
+  [[maybe_unused]] const int jsel = spers && nitems >= 3 ? nitems / 2 : 0;
+  int tsel = -1, jcur = 0;
   auto stamp = [&](int t, int k) {
     if constexpr (STAMPS) {
-      if (t == tsel) stp[k] = __builtin_amdgcn_s_memtime();
+      if (t == tsel && jcur == jsel) stp[k] = __builtin_amdgcn_s_memtime();
+      if (spers && t == 0 && jcur == jsel + 1 && (k == 4 || k == 5 || k == 10 || k == 11))
+        stp[16 + (k & 1) + (k >= 10 ? 2 : 0)] = __builtin_amdgcn_s_memtime();
     }
   };
   // one phase of global k-tile s (k-tile t of the current item): READ slot (fragments + the
   // streams' pieces, then vmcnt(<this phase's own loads>), so every older piece has landed
   // before the next phase), MMA slot (32 MFMAs)
-  auto phase = [&](auto Hc, int s, int t) {
+  // stores a wave issues in every non-WGRAD epilogue (at least): G16_DEFER's wait count
+  constexpr int NST = ((EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) && G16_DIAG_ST2) ? 32 : 16;
+  [[maybe_unused]] u32x4 bias4[4];
+  // tail: the item's last phase; its closing barrier is left to the caller (G16_EPI_SYNC)
+  auto phase = [&](auto Hc, int s, int t, bool defer, bool tail) {
     constexpr int H = decltype(Hc)::value;
     stamp(t, 2 + 6 * H);
     if constexpr (H == 0) {
@@ -638,7 +687,12 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
     issue_w(H);
     issue_x(H);
     stamp(t, 3 + 6 * H);
-    wait_vm_exact<4>();
+    if constexpr (H == 0 && G16_DEFER && EPI != EPI_WGRAD) {
+      if (defer) wait_vm_exact<4 + NST>();
+      else wait_vm_exact<4>();
+    } else {
+      wait_vm_exact<4>();
+    }
     stamp(t, 4 + 6 * H);
     g_barrier();
     stamp(t, 5 + 6 * H);
@@ -664,7 +718,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
       for (int b = 0; b < 4; ++b) acc[4 * H + a][b] = mfma16(Wf[a][1], X1[b], acc[4 * H + a][b]);
     __builtin_amdgcn_s_setprio(0);
     stamp(t, 7 + 6 * H);
-    g_barrier();
+    if (!tail) g_barrier();
   };
 
   // prologue: X k-tile 0 (B, C), W k-tile 0 (A, D), X k-tile 1 (B, C); phase (0, 0) needs the
@@ -685,27 +739,47 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
 
   int s = 0;
   for (int j = 0; j < nitems; ++j) {
-    const G16Item it = g16_decode(g, item_id(j));
-    if constexpr (STAMPS) tsel = it.nk / 2;
+    const G16Item it = decode(j);
+    if constexpr (STAMPS) {
+      tsel = it.nk / 2;
+      jcur = j;
+    }
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] = zero4();
     for (int t = 0; t < it.nk; ++t, ++s) {
-      phase(I0(), s, t);
-      phase(I1(), s, t);
+      phase(I0(), s, t, t == 0 && j > 0, false);
+      phase(I1(), s, t, false, t == it.nk - 1);
       advance_w();
       advance_x();
     }
-    if constexpr (STAMPS) stp[14] = __builtin_amdgcn_s_memtime();
-    g16_epilogue<EPI>(g, acc, it, wm, grp, q, i16);
+    // The last phase's closing barrier.  Group 1 runs one slot behind group 0: with the
+    // epilogue after that barrier in both groups (G16_EPI_SYNC 0) group 1 waits there through
+    // group 0's whole epilogue and group 0 then waits through group 1's at its next one -- the
+    // two epilogues run one after the other (scripts/gemm16_epi_stamps.py).  Group 1 runs its
+    // epilogue before the barrier instead, so both groups' epilogues fall between the same
+    // two barriers and run side by side.
+    const bool epi_first = G16_EPI_SYNC && grp == 1;
+    if (!epi_first) g_barrier();
+    if constexpr (STAMPS) {
+      if (j == jsel) stp[14] = __builtin_amdgcn_s_memtime();
+    }
+    g16_epilogue<EPI>(g, acc, it, wm, grp, q, i16, bias4);
+    if constexpr (STAMPS) {
+      if (spers && j == jsel) stp[15] = __builtin_amdgcn_s_memtime();
+    }
+    if (epi_first) g_barrier();
   }
   if (grp == 0) g_barrier();  // match group 1's barrier count
   wait_vm_exact<0>();         // the stream's last (dummy) LDS-DMA lands before the LDS is freed
   if constexpr (STAMPS) {
-    // 15: epilogue issued; 16: where the wave ran (HW_ID: cu / sh / se; XCC_ID); 17: its
-    // stores acknowledged (only with flags & 32, which waits for them: the default leaves the
-    // wave to end right after issuing, as the real kernel does)
+    // one item per workgroup: 15: epilogue issued; 16: where the wave ran (HW_ID: cu / sh /
+    // se; XCC_ID); 17: its stores acknowledged (only with flags & 32, which waits for them:
+    // the default leaves the wave to end right after issuing, as the real kernel does).
+    // Persistent (flags & 128): 15 the stamped item's epilogue issued, 16-19 the next item's
+    // first k-tile: phase 0 vmcnt retired, its barrier passed, phase 1 the same
+    if (!spers) {
     stp[15] = __builtin_amdgcn_s_memtime();
     stp[16] = (unsigned long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
               ((unsigned long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
@@ -714,17 +788,18 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stp[17] = __builtin_amdgcn_s_memtime();
     }
+    }
     if (lane == 0) {
       unsigned long* dst = reinterpret_cast<unsigned long*>(g.slabs) + ((long)blockIdx.x * 8 + wv) * 20;
 #pragma unroll
-      for (int k = 0; k < 18; ++k) dst[k] = stp[k];
+      for (int k = 0; k < 20; ++k) dst[k] = stp[k];
     }
   }
 }
 
 template <bool XKM, bool WKM, int EPI, bool STAMPS = false>
 static int gemm16_launch(const GemmArgs& a, hipStream_t st) {
-  if constexpr (!STAMPS && EPI == EPI_STORE) {
+  if constexpr (!STAMPS && (EPI == EPI_STORE || EPI == EPI_BIAS || EPI == EPI_BIAS_GELU)) {
     if ((a.flags & 4) && a.slabs) return gemm16_launch<XKM, WKM, EPI, true>(a, st);
   }
   static bool attr = false;
@@ -738,7 +813,7 @@ static int gemm16_launch(const GemmArgs& a, hipStream_t st) {
   if (work <= 0 || work > 0x7FFFFFFFL) return -1;
   // persistent walk (one workgroup per CU) unless a stamped diagnostic or flags & 64 asks for
   // one workgroup per item
-  const bool one_per_item = STAMPS || (a.flags & 64) || work <= 256;
+  const bool one_per_item = (STAMPS && !(a.flags & 128)) || (a.flags & 64) || work <= 256;
   const unsigned grid = one_per_item ? (unsigned)work : 256u;
   gemm16_kernel<XKM, WKM, EPI, STAMPS><<<grid, 512, G_LDS, st>>>(a);
   return (int)hipGetLastError();

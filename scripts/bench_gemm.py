@@ -66,7 +66,10 @@ def main():
               # 5: gemm_gelu_bwd (GELU'(pre + b) and the bias gradient in the epilogue) against
               # the unfused dgrad GEMM + bias_gelu_bwd (which also sums the bias gradient)
               ("mlpproj_dgrad+gelu_bwd+db", "dgrad", 3072, 768, 5),
-              ("lmhead_dgrad", "dgrad", 768, 50304, 0), ("lmhead_dgrad_rowscale", "dgrad", 768, 50304, 7)]
+              ("lmhead_dgrad", "dgrad", 768, 50304, 0), ("lmhead_dgrad_rowscale", "dgrad", 768, 50304, 7),
+              # the fused shapes without their epilogue arithmetic (price of the epilogue)
+              ("fc_fwd_plain", "fwd", 3072, 768, 0), ("fc_fwd+bias", "fwd", 3072, 768, 1),
+              ("mlpproj_dgrad_plain", "dgrad", 3072, 768, 0)]
     if a.llama:
         shapes = [("l_qkv_fwd", "fwd", 12288, 4096, 0), ("l_o_fwd", "fwd", 4096, 4096, 0),
                   ("l_gateup_fwd", "fwd", 22016, 4096, 0), ("l_down_fwd", "fwd", 4096, 11008, 0),
