@@ -38,7 +38,7 @@ int orion_wgrad_splits(int, int, int);
 int orion_wgrad_effective_splits(int, int);
 int orion_wgrad_tail_rows(int, int, int, int*);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
-                const float*, int, int, hipStream_t);
+                const float*, int, int, int, hipStream_t);
 int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
 int orion_sumsq_partials();
 int orion_grad_sumsq(const void*, long, int, float*, float*, hipStream_t);
@@ -65,7 +65,7 @@ int orion_lmhead_fold(const float*, int, const float*, const int64_t*, long, flo
                       const void*, long, const void*, long, int, float*, float*, float*, int*, int*, float*,
                       float*, hipStream_t);
 int orion_lmhead_bwd_prep(const void*, long, int, long, const int64_t*, long, int, const float*, const float*,
-                          const float*, float*, void*, hipStream_t);
+                          const float*, float*, void*, int, hipStream_t);
 int orion_gemm_set_diag(int flags);
 
 namespace {
@@ -447,9 +447,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lmhead_fwd(const Tensor& x, const Ten
   return {loss, E, invz, inv_n};
 }
 
-// Backward prologue: srow (N,) fp32 = g / (Z n_valid) on valid rows, xs (N, C) = srow (.) x.
+// Backward prologue: srow (N,) fp32 = g / (Z n_valid) on valid rows, xs (N, C) = srow (.) x
+// (transposed: xs is returned as (C, N), for the NT weight-gradient operand; N % 64 == 0 and
+// C % 64 == 0).
 std::tuple<Tensor, Tensor> lmhead_bwd_prep(const Tensor& x, const Tensor& targets, int64_t ignore_index,
-                                           int64_t V, const Tensor& invz, const Tensor& inv_n, const Tensor& g) {
+                                           int64_t V, const Tensor& invz, const Tensor& inv_n, const Tensor& g,
+                                           bool transposed) {
   check_bf16(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "lmhead_bwd_prep: x (N, C)");
   c10::hip::HIPGuardMasqueradingAsCUDA gd(x.device());
@@ -457,11 +460,12 @@ std::tuple<Tensor, Tensor> lmhead_bwd_prep(const Tensor& x, const Tensor& target
   const int Cd = (int)x.size(1);
   auto t = targets.contiguous();
   auto srow = at::empty({N}, x.options().dtype(at::kFloat));
-  auto xs = at::empty({N, (long)Cd}, x.options());
+  TORCH_CHECK(!transposed || (N % 64 == 0 && Cd % 64 == 0), "lmhead_bwd_prep: transposed needs N, C % 64 == 0");
+  auto xs = transposed ? at::empty({(long)Cd, N}, x.options()) : at::empty({N, (long)Cd}, x.options());
   auto gf = g.to(at::kFloat).reshape({1}).contiguous();
   check_launch(orion_lmhead_bwd_prep(x.data_ptr(), x.stride(0), Cd, N, t.data_ptr<int64_t>(), ignore_index, (int)V,
                                      invz.data_ptr<float>(), inv_n.data_ptr<float>(), gf.data_ptr<float>(),
-                                     srow.data_ptr<float>(), xs.data_ptr(), cur_stream()),
+                                     srow.data_ptr<float>(), xs.data_ptr(), transposed ? 1 : 0, cur_stream()),
                "lmhead_bwd_prep");
   return {srow, xs};
 }
@@ -522,14 +526,18 @@ Tensor slab_sum(const Tensor& slabs, const c10::optional<Tensor>& scale) {
 // dW = dy^T x over the token dim (csrc/wgrad.hip) into out (N1, N2) contiguous fp32 (the
 // gradient arena) or bf16: overwritten, or added to when accumulate (micro-batch
 // accumulation / tied weights).  splits = 0 picks the split-K count.
-void wgrad_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& scale, Tensor out,
+void wgrad_into(const Tensor& dy, const Tensor& x_in, const c10::optional<Tensor>& scale, Tensor out,
                 bool accumulate, int64_t splits) {
   check_bf16(dy, "dy");
-  check_bf16(x, "x");
+  check_bf16(x_in, "x");
   check_grad_out(out, "out");
-  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad: dy (M,N1), x (M,N2)");
-  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad: rows must be contiguous");
-  const int M = dy.size(0), N1 = dy.size(1), N2 = x.size(1);
+  TORCH_CHECK(dy.dim() == 2 && x_in.dim() == 2 && dy.size(0) == x_in.size(0), "wgrad: dy (M,N1), x (M,N2)");
+  const int M = dy.size(0), N1 = dy.size(1), N2 = x_in.size(1);
+  // x given as the transposed view of a row-major (N2, M) tensor: the NT-operand kernel
+  const bool xt = x_in.stride(0) == 1 && x_in.stride(1) != 1 && M % 64 == 0 && x_in.stride(1) % 8 == 0;
+  const Tensor x = (xt || x_in.stride(1) == 1) ? x_in : x_in.contiguous();
+  TORCH_CHECK(dy.stride(1) == 1, "wgrad: dy rows must be contiguous");
+  const long ldx = xt ? x.stride(1) : x.stride(0);
   TORCH_CHECK(out.is_contiguous() && out.numel() == (int64_t)N1 * N2, "wgrad: out must be contiguous (N1, N2)");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   int S = splits > 0 ? orion_wgrad_effective_splits(M, (int)splits) : orion_wgrad_splits(M, N1, N2);
@@ -541,27 +549,27 @@ void wgrad_into(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& 
   int S2 = 1;
   const int R1 = splits > 0 ? 0 : orion_wgrad_tail_rows(M, N1, N2, &S2);
   if (R1 > 0) {  // whole rounds unsplit, the tail rows split-K (orion_wgrad_tail_rows)
-    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, R1, N2, 1,
+    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), ldx, M, R1, N2, 1,
                              nullptr, out.data_ptr(), sc, accumulate ? 1 : 0, is_f32(out),
-                             cur_stream()), "wgrad head");
+                             xt ? 1 : 0, cur_stream()), "wgrad head");
     const int N1t = N1 - R1;
     auto slabs = at::empty({S2, N1t, N2}, dy.options().dtype(at::kFloat));
     const auto* dyt = static_cast<const char*>(dy.data_ptr()) + (size_t)R1 * dy.element_size();
     auto* outt = static_cast<char*>(out.data_ptr()) + (size_t)R1 * N2 * out.element_size();
-    check_launch(orion_wgrad(dyt, dy.stride(0), x.data_ptr(), x.stride(0), M, N1t, N2, S2,
-                             slabs.data_ptr<float>(), nullptr, nullptr, 0, 0, cur_stream()), "wgrad tail");
+    check_launch(orion_wgrad(dyt, dy.stride(0), x.data_ptr(), ldx, M, N1t, N2, S2,
+                             slabs.data_ptr<float>(), nullptr, nullptr, 0, 0, xt ? 1 : 0, cur_stream()), "wgrad tail");
     check_launch(orion_slab_sum(slabs.data_ptr<float>(), S2, (long)N1t * N2, outt, sc,
                                 accumulate ? 1 : 0, is_f32(out), cur_stream()), "wgrad tail slab_sum");
   } else if (S > 1) {
     auto slabs = at::empty({S, N1, N2}, dy.options().dtype(at::kFloat));
-    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, S,
-                             slabs.data_ptr<float>(), nullptr, nullptr, 0, 0, cur_stream()), "wgrad");
+    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), ldx, M, N1, N2, S,
+                             slabs.data_ptr<float>(), nullptr, nullptr, 0, 0, xt ? 1 : 0, cur_stream()), "wgrad");
     check_launch(orion_slab_sum(slabs.data_ptr<float>(), S, out.numel(), out.data_ptr(), sc,
                                 accumulate ? 1 : 0, is_f32(out), cur_stream()), "wgrad slab_sum");
   } else {
-    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N1, N2, 1,
+    check_launch(orion_wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), ldx, M, N1, N2, 1,
                              nullptr, out.data_ptr(), sc, accumulate ? 1 : 0, is_f32(out),
-                             cur_stream()), "wgrad");
+                             xt ? 1 : 0, cur_stream()), "wgrad");
   }
 }
 
@@ -572,6 +580,11 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& sca
 }
 
 int64_t wgrad_splits(int64_t M, int64_t N1, int64_t N2) { return orion_wgrad_splits(M, N1, N2); }
+std::tuple<int64_t, int64_t> wgrad_tail_rows(int64_t M, int64_t N1, int64_t N2) {
+  int s2 = 1;
+  const int r1 = orion_wgrad_tail_rows((int)M, (int)N1, (int)N2, &s2);
+  return {r1, s2};
+}
 
 // csrc/gemm.hip's diagnostic flags (stamps, one workgroup per work item): set in-process by
 // the benchmark / timeline scripts; returns the previous value
@@ -1019,10 +1032,11 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("wgrad(Tensor dy, Tensor x, Tensor? scale=None, int splits=0) -> Tensor");
   m.def("wgrad_into(Tensor dy, Tensor x, Tensor? scale, Tensor(a!) out, bool accumulate, int splits=0) -> ()");
   m.def("wgrad_splits(int M, int N1, int N2) -> int", &wgrad_splits);  // host-only helper
+  m.def("wgrad_tail_rows(int M, int N1, int N2) -> (int, int)", &wgrad_tail_rows);  // host-only
   m.def("gemm_diag(int flags) -> int", &gemm_diag);                   // host-only helper
   m.def("xent_fwd_bwd(Tensor(a!) logits, Tensor targets, int ignore_index) -> Tensor");
   m.def("lmhead_fwd(Tensor x, Tensor w, Tensor targets, int ignore_index, Tensor(a!) cref) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("lmhead_bwd_prep(Tensor x, Tensor targets, int ignore_index, int V, Tensor invz, Tensor inv_n, Tensor g) -> (Tensor, Tensor)");
+  m.def("lmhead_bwd_prep(Tensor x, Tensor targets, int ignore_index, int V, Tensor invz, Tensor inv_n, Tensor g, bool transposed=False) -> (Tensor, Tensor)");
   m.def("gemm_rowscale(Tensor e, Tensor w, Tensor srow) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");

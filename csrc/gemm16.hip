@@ -829,8 +829,9 @@ bool gemm16_ok(const GemmArgs& a, int wkm) {
   return band < lim && ob < lim && pb < lim && wb < lim;
 }
 
-int gemm16_wgrad(const GemmArgs& a, hipStream_t st) {
-  return gemm16_launch<true, true, EPI_WGRAD>(a, st);
+int gemm16_wgrad(const GemmArgs& a, int bt, hipStream_t st) {
+  // bt: the second operand NT ([N2][tokens], the LM head's transposed scaled activations)
+  return bt ? gemm16_launch<true, false, EPI_WGRAD>(a, st) : gemm16_launch<true, true, EPI_WGRAD>(a, st);
 }
 
 int gemm16(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {

@@ -83,6 +83,6 @@ ORION_DEVICE void g_wait_lds(bf16x8 (&a)[4][2]) {
 // gemm16_ok: the work item's 32-bit buffer offsets (one 256-row band, the whole k-major W)
 bool gemm16_ok(const GemmArgs& a, int wkm);
 int gemm16(const GemmArgs& a, int wkm, int epi, hipStream_t st);
-int gemm16_wgrad(const GemmArgs& a, hipStream_t st);
+int gemm16_wgrad(const GemmArgs& a, int bt, hipStream_t st);
 
 }  // namespace orion

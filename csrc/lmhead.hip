@@ -163,6 +163,45 @@ __global__ __launch_bounds__(256) void lmhead_bwd_prep_kernel(
   *reinterpret_cast<bf16x8*>(Xs + row * Cdim + k) = o;
 }
 
+// The same with Xs written transposed, XsT [Cdim][N] (N % 64 == 0, Cdim % 64 == 0): the
+// weight gradient dW = E'^T Xs then reads Xs as an NT operand (one ds_read_b128 per fragment
+// instead of two transposing reads, csrc/wgrad.hip orion_wgrad_nt).  One 64-row x 64-column
+// block per workgroup, transposed through LDS.
+__global__ __launch_bounds__(256) void lmhead_bwd_prep_t_kernel(
+    const bf16_t* __restrict__ X, long ldx, long N, const int64_t* __restrict__ tgt, long ignore, int V,
+    const float* __restrict__ invz, const float* __restrict__ inv_n, const float* __restrict__ g,
+    float* __restrict__ srow, bf16_t* __restrict__ XsT) {
+  __shared__ bf16_t tile[64][64 + 8];  // [column][row]
+  const int tid = threadIdx.x;
+  const long r0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  {
+    const int r = tid >> 2, cc = (tid & 3) * 16;
+    const long row = r0 + r;
+    const float sv = lm_valid(tgt[row], ignore, V) ? g[0] * inv_n[0] * invz[row] : 0.f;
+    if (blockIdx.y == 0 && (tid & 3) == 0) srow[row] = sv;
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(X + row * ldx + c0 + cc);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bf16x8 x = src[h];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[cc + 8 * h + j][r] = f2bf(bf2f(x[j]) * sv);
+    }
+  }
+  __syncthreads();
+  {
+    const int c = tid >> 2, rr = (tid & 3) * 16;
+    bf16x8* dst = reinterpret_cast<bf16x8*>(XsT + (long)(c0 + c) * N + r0 + rr);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = tile[c][rr + 8 * h + j];
+      dst[h] = o;
+    }
+  }
+}
+
 }  // namespace orion
 
 using namespace orion;
@@ -185,9 +224,16 @@ int orion_lmhead_fold(const float* part, int npart, const float* tlog, const int
   return (int)hipGetLastError();
 }
 
+// transposed != 0: Xs is written as XsT [Cdim][N] (needs N % 64 == 0 and Cdim % 64 == 0)
 int orion_lmhead_bwd_prep(const void* X, long ldx, int Cdim, long N, const int64_t* tgt, long ignore,
                           int V, const float* invz, const float* inv_n, const float* g, float* srow,
-                          void* Xs, hipStream_t st) {
+                          void* Xs, int transposed, hipStream_t st) {
+  if (transposed) {
+    if (N % 64 || Cdim % 64 || ldx % 8 || N / 64 > 0x7FFFFFFFL) return -1;
+    lmhead_bwd_prep_t_kernel<<<dim3((unsigned)(N / 64), (unsigned)(Cdim / 64)), 256, 0, st>>>(
+        (const bf16_t*)X, ldx, N, tgt, ignore, V, invz, inv_n, g, srow, (bf16_t*)Xs);
+    return (int)hipGetLastError();
+  }
   if (Cdim % 8) return -1;
   const long n = N * (Cdim / 8);
   lmhead_bwd_prep_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(

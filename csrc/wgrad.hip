@@ -212,25 +212,28 @@ int orion_wgrad_splits(int M, int N1, int N2) {
 }
 
 // Tail split of an unsplit weight gradient whose tile count leaves a partial last round
-// (one workgroup per CU, 256 CUs): the first R1 output rows form whole rounds and run
-// unsplit; the remaining rows -- at most half a round of tiles -- run split-K over S2 =
-// 256 / tail-tiles chunks, so the last round costs 1 / S2 of an item instead of a whole one.
+// (one workgroup per CU, 256 CUs): the first R1 output rows -- the whole rows of tiles that
+// fit in the whole rounds -- run unsplit; the remaining rows (at most ~half a round of tiles,
+// the last row of tiles may be partial) run split-K over S2 = 256 / tail-tiles chunks, so the
+// last round costs about 1 / S2 of an item instead of a whole one.
 // Llama-7B gate_up (22,016 x 4,096: 1,376 tiles, 5.4 rounds): 80 rows of tiles unsplit +
-// 6 rows at S2 = 2 -- 5.5 instead of 6 item times.  Returns R1 (0: no split) and S2.
+// 6 rows at S2 = 2 -- 5.5 instead of 6 item times.  GPT-2's LM head (50,304 x 768: 591
+// tiles, 2.3 rounds, round 5): 170 rows unsplit (510 tiles) + 26.5 rows at S2 = 3 -- 2.33
+// instead of 3 item times.  Returns R1 (0: no split) and S2.
 int orion_wgrad_effective_splits(int M, int S);
 
 int orion_wgrad_tail_rows(int M, int N1, int N2, int* S2) {
   *S2 = 1;
-  if (orion_wgrad_splits(M, N1, N2) != 1 || N1 % 256) return 0;
-  const long t1 = N1 / 256, t2 = (N2 + 255) / 256, tiles = t1 * t2;
-  const long rem = tiles % 256;
-  if (tiles <= 256 || rem == 0 || rem > 128) return 0;
-  const long head = tiles - rem;
-  if (head % t2) return 0;  // the whole rounds must be whole rows of tiles
+  if (orion_wgrad_splits(M, N1, N2) != 1) return 0;
+  const long t1 = (N1 + 255) / 256, t2 = (N2 + 255) / 256, tiles = t1 * t2;
+  if (tiles <= 256 || tiles % 256 == 0) return 0;
+  const long head_rows = (tiles / 256) * 256 / t2;  // whole tile rows inside the whole rounds
+  const long rem = tiles - head_rows * t2;
+  if (head_rows < 1 || head_rows >= t1 || rem > 128) return 0;
   const int s2 = orion_wgrad_effective_splits(M, (int)(256 / rem));
   if (s2 < 2) return 0;
   *S2 = s2;
-  return (int)(head / t2) * 256;
+  return (int)head_rows * 256;
 }
 
 // number of k-chunks actually produced when S are requested (chunks are whole stages)
@@ -243,12 +246,15 @@ int orion_wgrad_effective_splits(int M, int S) {
 
 // A (M x N1, ld lda), B (M x N2, ld ldb) bf16 -> slabs (S, N1, N2) fp32 when S > 1
 // (caller folds them), else out (N1, N2; fp32 when out_f32, else bf16) scaled by *scale
-// (nullable), added to the values already in out when accumulate != 0.
+// (nullable), added to the values already in out when accumulate != 0.  bt != 0: B is given
+// transposed, (N2 x M, ld ldb) -- the NT operand of gemm16 (one ds_read_b128 per fragment
+// instead of two transposing reads; M % 64 == 0).
 int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1, int N2, int S,
-                float* slabs, void* out, const float* scale, int accumulate, int out_f32,
+                float* slabs, void* out, const float* scale, int accumulate, int out_f32, int bt,
                 hipStream_t st) {
   const int BK = wg_bk(M);
   if (M % BK || N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || N1 < 8 || N2 < 8) return -1;
+  if (bt && BK != 64) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -2;
   const int chunk = ((M / BK + S - 1) / S) * BK;
   const int Se = (M + chunk - 1) / chunk;
@@ -256,11 +262,14 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
   if (S > 1 && !slabs) return -4;
   const int t1 = (N1 + 255) / 256, t2 = (N2 + 255) / 256;
   const int ntiles = t1 * t2;
-  if (BK == 64 && (long)chunk * (lda > ldb ? lda : ldb) * 2 < 0xFFFFFF00L) {
+  const long lim = 0xFFFFFF00L;
+  const bool fits = (long)chunk * lda * 2 < lim && (bt ? 256L * ldb * 2 : (long)chunk * ldb * 2) < lim;
+  if (bt && !fits) return -1;
+  if (BK == 64 && fits) {
     GemmArgs a{};
     a.X = (const bf16_t*)A;  // [M tokens][N1]: the k-major "X" operand, rows of out = N1
     a.ldx = lda;
-    a.W = (const bf16_t*)B;  // [M tokens][N2]
+    a.W = (const bf16_t*)B;  // [M tokens][N2], or (bt) [N2][M tokens]
     a.ldw = ldb;
     a.out = (bf16_t*)out;
     a.ldo = N2;
@@ -274,7 +283,7 @@ int orion_wgrad(const void* A, long lda, const void* B, long ldb, int M, int N1,
     a.scale = scale;
     a.accumulate = accumulate;
     a.out_f32 = out_f32;
-    return gemm16_wgrad(a, st);
+    return gemm16_wgrad(a, bt, st);
   }
   constexpr int lds = WG_NS * WG_KS * 16 * 128 * 4 * (int)sizeof(bf16_t);
   static bool attr = false;

@@ -164,10 +164,13 @@ _IMPL = os.environ.get("ORION_WGRAD", "hip")  # "hip" (csrc/gemm16.hip) | "blas"
 
 
 def _hip_ok(dy, x):
+    # x row-major (M, n2), or the transposed view of a row-major (n2, M) tensor (the NT-operand
+    # kernel, M % 64 == 0)
+    x_rows = x.stride(1) == 1 and x.stride(0) % 8 == 0
+    x_t = x.stride(0) == 1 and x.stride(1) % 8 == 0 and dy.shape[0] % 64 == 0
     return (_IMPL == "hip" and dy.is_cuda and dy.shape[0] % 32 == 0 and dy.shape[1] % 8 == 0
-            and x.shape[1] % 8 == 0 and dy.stride(1) == 1 and x.stride(1) == 1
-            and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0
-            and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
+            and x.shape[1] % 8 == 0 and dy.stride(1) == 1 and (x_rows or x_t)
+            and dy.stride(0) % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
 def wgrad_splits(M: int, n1: int, n2: int) -> int:

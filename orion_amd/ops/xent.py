@@ -63,6 +63,9 @@ def linear_cross_entropy_hip(x, w, targets, ignore_index=-1):
 
 
 _LMHEAD = os.environ.get("ORION_LMHEAD", "exp")
+# the scaled activations of the LM-head weight gradient written transposed (C, N), so the
+# weight gradient reads them as an NT operand (csrc/wgrad.hip, bt); ORION_LMHEAD_XT=0: (N, C)
+_LM_XT = os.environ.get("ORION_LMHEAD_XT", "1") == "1"
 _CREF = {}
 
 
@@ -103,7 +106,10 @@ class _LinearXentExp(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, w, t, e, invz, inv_n = ctx.saved_tensors
-        srow, xs = C().lmhead_bwd_prep(x, t, ctx.ignore, w.shape[0], invz, inv_n, g.detach())
+        xt = _LM_XT and x.shape[0] % 64 == 0 and x.shape[1] % 64 == 0
+        srow, xs = C().lmhead_bwd_prep(x, t, ctx.ignore, w.shape[0], invz, inv_n, g.detach(), xt)
+        if xt:
+            xs = xs.t()  # (N, C) view of the (C, N) tensor
         one = torch.ones(1, dtype=torch.float32, device=x.device)
         dx = dw = None
         if ctx.needs_input_grad[0] and not _LM_WGRAD_FIRST:

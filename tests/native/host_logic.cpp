@@ -14,7 +14,7 @@ int orion_wgrad_splits(int M, int N1, int N2);
 int orion_wgrad_effective_splits(int M, int S);
 int orion_wgrad_tail_rows(int M, int N1, int N2, int* S2);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
-                const float*, int, int, hipStream_t);
+                const float*, int, int, int, hipStream_t);
 int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, void*, long,
                const void*, void*, long, const void*, long, hipStream_t, void* db = nullptr,
                int db_f32 = 0, float* part = nullptr);
@@ -47,7 +47,8 @@ int main() {
           CHECK(e >= 1 && e <= req);
         }
       }
-  // tail split: head rows are whole rounds of whole tile rows, the tail at most half a round
+  // tail split: head rows are the whole tile rows inside the whole rounds, the tail (a partial
+  // last tile row allowed) at most half a round
   for (int M : Ms)
     for (int n1 : Ns)
       for (int n2 : Ns) {
@@ -55,8 +56,9 @@ int main() {
         const int R1 = orion_wgrad_tail_rows(M, n1, n2, &S2);
         CHECK(R1 >= 0 && R1 < n1 && R1 % 256 == 0);
         if (R1 > 0) {
-          const long t2 = (n2 + 255) / 256, head = (long)(R1 / 256) * t2, tail = (long)(n1 - R1) / 256 * t2;
-          CHECK(head % 256 == 0 && tail > 0 && tail <= 128);
+          const long t1 = (n1 + 255) / 256, t2 = (n2 + 255) / 256, tiles = t1 * t2;
+          const long head = (long)(R1 / 256) * t2, tail = tiles - head, whole = tiles / 256 * 256;
+          CHECK(head <= whole && head > whole - t2 && tail > 0 && tail <= 128);
           CHECK(S2 >= 2 && tail * S2 <= 256 && orion_wgrad_effective_splits(M, S2) == S2);
         } else {
           CHECK(S2 == 1);
@@ -66,6 +68,8 @@ int main() {
     int S2 = 0;
     CHECK(orion_wgrad_tail_rows(16384, 22016, 4096, &S2) == 80 * 256 && S2 == 2);
     CHECK(orion_wgrad_tail_rows(16384, 12288, 4096, &S2) == 0);  // 768 tiles: whole rounds
+    // GPT-2's LM head at 4k tokens: 170 tile rows unsplit, 26.5 rows at S2 = 3
+    CHECK(orion_wgrad_tail_rows(4096, 50304, 768, &S2) == 170 * 256 && S2 == 3);
   }
   // scratch sizing is monotone and positive
   for (int rows = 1; rows < (1 << 20); rows = rows * 3 + 1) {
@@ -94,9 +98,9 @@ int main() {
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 3, o, 64, nullptr, nullptr, 0, p, 64, 0, o, 0, nullptr) == -3);  // db needs scratch
   CHECK(orion_gemm(p, 64, p, 64, 64, 64, 64, 1, 3, o, 72, nullptr, nullptr, 0, p, 64, 0, o, 0, part) == -3);     // db needs ldo == N
   CHECK(orion_gemm_colsum_scratch(65, 64) == (2 + 32) * 64);
-  CHECK(orion_wgrad(p, 64, p, 64, 33, 64, 64, 1, nullptr, o, nullptr, 0, 0, 0) == -1);                 // M % BK
-  CHECK(orion_wgrad(mis, 64, p, 64, 64, 64, 64, 1, nullptr, o, nullptr, 0, 0, 0) == -2);               // alignment
-  CHECK(orion_wgrad(p, 64, p, 64, 4096, 64, 64, 2, nullptr, o, nullptr, 0, 0, 0) == -4);               // slabs missing
+  CHECK(orion_wgrad(p, 64, p, 64, 33, 64, 64, 1, nullptr, o, nullptr, 0, 0, 0, 0) == -1);              // M % BK
+  CHECK(orion_wgrad(mis, 64, p, 64, 64, 64, 64, 1, nullptr, o, nullptr, 0, 0, 0, 0) == -2);            // alignment
+  CHECK(orion_wgrad(p, 64, p, 64, 4096, 64, 64, 2, nullptr, o, nullptr, 0, 0, 0, 0) == -4);            // slabs missing
   if (failures) return 1;
   std::printf("host logic ok\n");
   return 0;

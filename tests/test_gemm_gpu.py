@@ -198,18 +198,40 @@ def test_wgrad_into_fp32(M, N1, N2, acc, gemm_cfg):
     assert rel_err(out, want) < 1e-4
 
 
-def test_wgrad_tail_split_bf16_scaled():
+@pytest.mark.parametrize("M,N1,N2,R1", [(2048, 22016, 4096, 20480), (4096, 50304, 768, 43520)])
+def test_wgrad_tail_split_bf16_scaled(M, N1, N2, R1):
     """The tail-split weight gradient into a bf16 output with a device scale: head rows and
-    tail rows both scaled once (the head in its epilogue, the tail in the slab sum)."""
+    tail rows both scaled once (the head in its epilogue, the tail in the slab sum).  Llama's
+    gate_up (whole tile rows), GPT-2's LM head (591 tiles: 170 rows unsplit, the last 26.5
+    rows -- a partial row of tiles among them -- split-K over 3 chunks)."""
     g = torch.Generator(device=DEV).manual_seed(7)
-    M, N1, N2 = 2048, 22016, 4096
     assert _C().wgrad_splits(M, N1, N2) == 1
+    assert _C().wgrad_tail_rows(M, N1, N2)[0] == R1
     dy, x = _rnd(g, M, N1), _rnd(g, M, N2)
     sc = torch.tensor([0.25], device=DEV)
     out = _C().wgrad(dy, x, sc, 0)
     want = (dy.float().t() @ x.float()) * 0.25
     within_bf16_budget("dw", out, want, ((dy.t() @ x).float() * 0.25).bfloat16())
-    assert rel_err(out[:20480], want[:20480]) < 5e-3 and rel_err(out[20480:], want[20480:]) < 5e-3
+    assert rel_err(out[:R1], want[:R1]) < 5e-3 and rel_err(out[R1:], want[R1:]) < 5e-3
+
+
+@pytest.mark.parametrize("M,N1,N2", [(4096, 768, 768), (8192, 2304, 768), (4096, 50304, 768), (1024, 1000, 264)])
+def test_wgrad_transposed_x_matches(M, N1, N2, gemm_cfg):
+    """x given as the transposed view of a row-major (N2, M) tensor takes the NT-operand
+    weight-gradient kernel (the LM head's scaled activations, csrc/lmhead.hip): fp32 arena
+    output against fp32 (split-K, tail split and ragged shapes), and bitwise equal to the
+    k-major form on the same data (same fragments, same MFMA order)."""
+    g = torch.Generator(device=DEV).manual_seed(M + N1 + N2)
+    dy, x = _rnd(g, M, N1), _rnd(g, M, N2)
+    xt = x.t().contiguous().t()  # (M, N2) view, stride (1, M)
+    assert xt.stride(0) == 1
+    out_t = torch.zeros(N1, N2, device=DEV)
+    out_k = torch.zeros(N1, N2, device=DEV)
+    _C().wgrad_into(dy, xt, None, out_t, False, 0)
+    _C().wgrad_into(dy, x, None, out_k, False, 0)
+    want = dy.float().t() @ x.float()
+    assert rel_err(out_t, want) < 1e-4
+    assert torch.equal(out_t, out_k)
 
 
 @pytest.mark.parametrize("wkm", [False, True])

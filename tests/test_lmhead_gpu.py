@@ -86,6 +86,25 @@ def test_lmhead_exp_vs_rowpass_forms():
                                                                               rel_err(b[i], want[i]))
 
 
+def test_lmhead_transposed_wgrad_operand_is_bitwise_equal():
+    """ORION_LMHEAD_XT (default): the backward prologue writes the scaled activations
+    transposed and the weight gradient reads them as an NT operand; dW and dX are bitwise
+    equal to the (N, C) form."""
+    V, C, N = 50304, 768, 1024
+    x, w, t = _case(N, V, C, True, seed=11)
+    res = []
+    old = X._LM_XT
+    try:
+        for xt in (True, False):
+            X._LM_XT = xt
+            X._cref(x.device).zero_()
+            res.append(_run(x, w, t, 1.0))
+    finally:
+        X._LM_XT = old
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+
+
 def test_lmhead_fixup_every_row_and_reference_update():
     """A reference far above every logit underflows every row: the fold flags all of them,
     the GEMV fixup recomputes them with their own maxima, and the results stay within the
