@@ -638,6 +638,202 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   }
 }
 
+// ============================================================================ dQ, 4 waves/SIMD
+// attn_bwd_dq4 (round 5, D = 64): the dQ kernel on attn_fwd4's recipe (csrc/attn_fwd.hip).
+// The round-2..4 kernel above stages K / V through registers (gload / swrite) and leaves its
+// LDS reads to the compiler: 150-156 VGPRs, three waves per SIMD.  Here K / V tiles arrive by
+// LDS-DMA into a double buffer, every fragment read is inline asm at an immediate offset with
+// a counted wait, and the chains run one after the other on shared fragment registers
+// (S^T: K fragments; dP^T: V fragments; dQ^T: K^T halves), so the live set is Q and dO
+// fragments 32, dQ 32, S / P 16, dP / dS 16 and one chain's fragments 16: under 128 VGPRs,
+// four workgroups of 4 waves per CU (32 KB of LDS each).  Same numerics as attn_bwd_dq.
+template <bool CAUSAL, bool BIAS>
+__global__ __launch_bounds__(256, 4) void attn_bwd_dq4_kernel(AttnParams p) {
+  constexpr int D = 64, BM = 128, BN = 64, TILE = BN * D, NDB = 2;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int BH = p.B * p.Hq;
+  const int nqt = (p.T + BM - 1) / BM;
+  const int bh = blockIdx.x % BH;
+  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) tiles launch first
+  const int b = bh / p.Hq, hq = bh % p.Hq, hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qt * BM, qw0 = q0 + wv * 32, myq = qw0 + l32;
+  const int off = p.Tk - p.T;
+  const float c = p.scale_log2;
+
+  const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
+
+  // Q and dO fragments of this wave's 32 queries (B operands of S^T = K Q^T, dP^T = V dO^T)
+  bf16x8 qf[D / 16], df[D / 16];
+  float L, dl;
+  {
+    const int qr = min(myq, p.T - 1);
+    const bf16_t* Qr = p.q + b * p.q_sb + hq * p.q_sh + (long)qr * p.q_st;
+    const bf16_t* Dr = p.dout + b * p.do_sb + hq * p.do_sh + (long)qr * p.do_st;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Qr + ks * 16 + 8 * h32);
+      df[ks] = *reinterpret_cast<const bf16x8*>(Dr + ks * 16 + 8 * h32);
+    }
+    const long r = ((long)b * p.Hq + hq) * p.T + qr;
+    L = p.lse[r];
+    dl = p.delta[r];
+  }
+  const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
+  const int ntiles = (kend + BN - 1) / BN;
+
+  // LDS-DMA of K / V tiles as attn_fwd4_kernel: 8 pieces of 8 rows x 128 bytes per image, wave
+  // wv issues pieces 2 wv, 2 wv + 1; the swizzle rides on the source chunk
+  const unsigned kst_b = (unsigned)p.k_st * 2, vst_b = (unsigned)p.v_st * 2;
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc(Kb, (unsigned)((long)(p.Tk - 1) * p.k_st + D) * 2);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(Vb, (unsigned)((long)(p.Tk - 1) * p.v_st + D) * 2);
+  const int prow0 = 16 * wv + (lane >> 3);
+  auto dma = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    bf16_t* Ks = smem + buf * 2 * TILE;
+    const int k0 = t * BN;
+    // the per-lane source offsets are recomputed per call (opaque row): hoisted, the four of
+    // them were spilled in the causal kernels
+    int pr = prow0;
+    asm volatile("" : "+v"(pr));
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = pr + 8 * e;
+      const unsigned ch16 = 16u * (unsigned)((lane & 7) ^ swz<D>(row));
+      if (k0 + BN <= p.Tk) {
+        blds16(rk, (unsigned)row * kst_b + ch16, (unsigned)k0 * kst_b, Ks + (2 * wv + e) * 512);
+        blds16(rv, (unsigned)row * vst_b + ch16, (unsigned)k0 * vst_b, Ks + TILE + (2 * wv + e) * 512);
+      } else {  // last partial tile: rows past Tk re-read the last key (masked below)
+        const unsigned key = (unsigned)min(k0 + row, p.Tk - 1);
+        blds16(rk, key * kst_b + ch16, 0, Ks + (2 * wv + e) * 512);
+        blds16(rv, key * vst_b + ch16, 0, Ks + TILE + (2 * wv + e) * 512);
+      }
+    }
+  };
+  // per-lane LDS byte bases: K / V rows l32 at d chunk 2 ks + h32 (the 32-key block by an
+  // immediate); K^T transposed reads of key rows 4 h32 + (iq >> 2) (+ 8: second half), columns
+  // db 32 + 16 (gq & 1) + 4 (iq & 3) (the 16-key step by an immediate: the swizzle does not
+  // depend on it)
+  // Registers are the budget here: one relative base per read family, the chunk index of
+  // fragment ks / block db applied by an xor per read (loff's swizzle is an xor on the 16-byte
+  // chunk: fragment ks is chunk (2 ks) ^ z, d block db flips chunk bit 2), kept opaque per
+  // block so the compiler does not hoist the four addresses back into registers.
+  const unsigned lds0 = lds_addr(smem, 0);
+  const unsigned zk = 2u * (unsigned)loff<D>(l32, 8 * h32);  // fragment 0 (chunk h32 ^ swz)
+  const int gq = lane >> 4, iq = lane & 15;
+  unsigned ztr[2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+    ztr[hf] = 2u * (unsigned)loff<D>(4 * h32 + (iq >> 2) + 8 * hf, 16 * (gq & 1) + 4 * (iq & 3));
+  // key k0 + rowoff(r) + 4 h32 of a 32-key block is visible to this lane's query iff
+  // rowoff(r) <= vis - k0
+  const int vis = (CAUSAL ? min(myq + off, p.Tk - 1) : p.Tk - 1) - 4 * h32;
+
+  f32x16 dq[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) dq[db] = zero16();
+
+  // one 32-key block (kb) of the tile in buffer BUF
+  auto block = [&](int t, auto bufc, auto kbc) {
+    constexpr int buf = decltype(bufc)::value, kb = decltype(kbc)::value;
+    constexpr unsigned BOFF = buf * 2 * TILE * 2 + kb * 32 * D * 2;  // bytes: K block
+    const int k0 = t * BN + kb * 32;
+    if (CAUSAL && k0 > qw0 + 31 + off) return;  // wave-uniform: block fully masked
+    f32x16 s = zero16(), dp = zero16();
+    unsigned zb = zk, zt0 = ztr[0], zt1 = ztr[1];
+    asm volatile("" : "+v"(zb), "+v"(zt0), "+v"(zt1));
+    auto kad = [&](int ks) { return lds0 + (zb ^ (unsigned)(ks << 5)); };
+    // S^T then dP^T on the same fragment registers
+    auto chain = [&](f32x16& acc, const bf16x8 (&bop)[D / 16], auto offc) {
+      constexpr unsigned O = decltype(offc)::value;
+      // all four reads in flight; the MFMAs wait for them in order (reading two at a time
+      // measured the same: 0.555-0.559 vs 0.554-0.558 ms)
+      bf16x8 f[4];
+      f[0] = b128_read_at<O>(kad(0));
+      f[1] = b128_read_at<O>(kad(1));
+      f[2] = b128_read_at<O>(kad(2));
+      f[3] = b128_read_at<O>(kad(3));
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(f[0]), "+v"(f[1]));
+      mfma_prio(true);
+      acc = mfma32(f[0], bop[0], acc);
+      acc = mfma32(f[1], bop[1], acc);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[2]), "+v"(f[3]));
+      acc = mfma32(f[2], bop[2], acc);
+      acc = mfma32(f[3], bop[3], acc);
+      mfma_prio(false);
+    };
+    chain(s, qf, std::integral_constant<unsigned, BOFF>{});
+    chain(dp, df, std::integral_constant<unsigned, BOFF + TILE * 2>{});
+    // S^T / dP^T: row = key k0 + (r&3)+8(r>>2)+4*h32, column = this lane's query
+    const bool need_mask = (CAUSAL && (k0 + 31 > qw0 + off)) || (k0 + 32 > p.Tk);
+    if (need_mask) {
+      const int lim = vis - k0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = ((r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c, -L));
+      dp[r] = pv * (dp[r] - dl);  // dS^T / scale
+    }
+    const bf16x8 ds0 = acc_to_frag(dp, 0), ds1 = acc_to_frag(dp, 1);
+    // dQ^T += K^T dS^T: K^T by transposed reads, kept as halves until their wait
+    constexpr unsigned T0 = buf * 2 * TILE * 2 + (2 * kb) * 16 * D * 2, T1 = T0 + 16 * D * 2;
+    bf16x4 lo[NDB][2], hi[NDB][2];
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      const unsigned a0 = lds0 + (zt0 ^ (unsigned)(db << 6)), a1 = lds0 + (zt1 ^ (unsigned)(db << 6));
+      lo[db][0] = tr_read_at<T0>(a0);
+      hi[db][0] = tr_read_at<T0>(a1);
+      lo[db][1] = tr_read_at<T1>(a0);
+      hi[db][1] = tr_read_at<T1>(a1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(lo[0][0]), "+v"(lo[0][1]), "+v"(lo[1][0]), "+v"(lo[1][1]), "+v"(hi[0][0]),
+                   "+v"(hi[0][1]), "+v"(hi[1][0]), "+v"(hi[1][1]));
+    mfma_prio(true);
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      dq[db] = mfma32(cat8(lo[db][0], hi[db][0]), ds0, dq[db]);
+      dq[db] = mfma32(cat8(lo[db][1], hi[db][1]), ds1, dq[db]);
+    }
+    mfma_prio(false);
+  };
+  auto tile = [&](int t, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    // tile t landed (this wave's pieces; the barrier: everyone's) and every wave is done with
+    // the other buffer (read in tile t - 1): tile t + 1 may overwrite it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < ntiles) dma(t + 1, std::integral_constant<int, buf ^ 1>{});
+    block(t, bufc, std::integral_constant<int, 0>{});
+    block(t, bufc, std::integral_constant<int, 1>{});
+  };
+
+  if (ntiles > 0) dma(0, std::integral_constant<int, 0>{});
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the workgroup ends
+
+  if (BIAS && qw0 < p.T)  // column sums of this wave's 32 queries (packed QKV bias grad)
+    wave_colsum_store<NDB>(dq, p.scale, myq < p.T, l32, h32,
+                           p.bias_part + ((long)b * ((p.T + 31) / 32) + qw0 / 32) * p.bias_ld + hq * D);
+  if (myq < p.T) {
+    ORION_DASSERT(b < p.B && hq < p.Hq);
+    bf16_t* Qo = p.dq + b * p.dq_sb + hq * p.dq_sh + (long)myq * p.dq_st;
+    const long rrow = (long)(myq + p.rope_pos0) * (D / 2);
+    store_row_grad<NDB>(dq, p.scale, Qo, h32, p.rope_cos ? p.rope_cos + rrow : nullptr,
+                        p.rope_sin ? p.rope_sin + rrow : nullptr);
+  }
+}
+
 }  // namespace orion
 
 using namespace orion;
@@ -660,8 +856,32 @@ static void kv_launch(const AttnParams& q, int grid, hipStream_t st) {
   attn_bwd_kv_kernel<D, CAUSAL><<<grid, kv_waves<D>() * 64, kv_lds(D), st>>>(q);
 }
 
+// ORION_ATTN_DQ=v3: the D = 64 dQ kernel of rounds 2-4 (A/B); default attn_bwd_dq4
+static bool dq_v3() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORION_ATTN_DQ");
+    v = (e && strcmp(e, "v3") == 0) ? 1 : 0;
+  }
+  return v == 1;
+}
+
+template <bool CAUSAL, bool BIAS>
+static void dq4_launch(const AttnParams& q, int grid, hipStream_t st) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq4_kernel<CAUSAL, BIAS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 64 * 64 * 2);
+    done = true;
+  }
+  attn_bwd_dq4_kernel<CAUSAL, BIAS><<<grid, 256, 2 * 2 * 64 * 64 * 2, st>>>(q);
+}
+
 template <int D, bool CAUSAL, bool BIAS = false>
 static void dq_launch(const AttnParams& q, int grid, hipStream_t st) {
+  if constexpr (D == 64) {
+    if (!dq_v3()) return dq4_launch<CAUSAL, BIAS>(q, grid, st);
+  }
   static bool done = false;
   if (!done) {
     (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, BIAS>,

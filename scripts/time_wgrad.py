@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Time the weight-gradient GEMM (csrc/wgrad.hip via gemm16) on one shape, x row-major vs
-x given as the transposed view of a (N2, M) tensor (the NT-operand kernel), interleaved.
+x given as the transposed view of a (N2, M) tensor (the NT-operand kernel), and hipBLASLt
+(fp32 output), interleaved.
 usage: python scripts/time_wgrad.py [M N1 N2] [iters]"""
 import json
 import os
@@ -20,7 +21,8 @@ x = torch.randn(M, N2, device="cuda", generator=g).bfloat16()
 xt = x.t().contiguous().t()
 out = torch.zeros(N1, N2, device="cuda")
 fns = {"kmajor": lambda: C().wgrad_into(dy, x, None, out, False, 0),
-       "nt": lambda: C().wgrad_into(dy, xt, None, out, False, 0)}
+       "nt": lambda: C().wgrad_into(dy, xt, None, out, False, 0),
+       "blas": lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)}
 ts = {k: [] for k in fns}
 for f in fns.values():
     f()
