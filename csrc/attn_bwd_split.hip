@@ -96,15 +96,11 @@ ORION_DEVICE bf16x8 bwd_buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsi
 // of l32 and adds its partner's copy of it): 31 shuffles for 32 values instead of a
 // butterfly per value.  Lane l32 ends with values l32 * (NV / 32) + j, written to
 // dst[d(value)]; rows past the end contribute 0 (valid = false).
-template <int NDB>
-ORION_DEVICE void wave_colsum_store(const f32x16 (&x)[NDB], float sc, bool valid, int l32, int h32,
-                                    float* __restrict__ dst) {
-  constexpr int NV = 16 * NDB;
-  float v[NV];
-#pragma unroll
-  for (int db = 0; db < NDB; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[16 * db + r] = valid ? x[db][r] * sc : 0.f;
+// The halving exchange of wave_colsum_store on NV values per lane (NV a multiple of 32):
+// afterwards v[j] (j < NV / 32) holds the sum over the 32 lanes of one h32 half of value index
+// l32 * (NV / 32) + j.
+template <int NV>
+ORION_DEVICE void wave_colsum_vals(float (&v)[NV], int l32) {
   auto step = [&](auto Oc, auto Lc) {
     constexpr int o = decltype(Oc)::value, L = decltype(Lc)::value, half = L / 2;
     const bool up = (l32 & o) != 0;
@@ -120,6 +116,18 @@ ORION_DEVICE void wave_colsum_store(const f32x16 (&x)[NDB], float sc, bool valid
   step(std::integral_constant<int, 4>(), std::integral_constant<int, NV / 4>());
   step(std::integral_constant<int, 2>(), std::integral_constant<int, NV / 8>());
   step(std::integral_constant<int, 1>(), std::integral_constant<int, NV / 16>());
+}
+
+template <int NDB>
+ORION_DEVICE void wave_colsum_store(const f32x16 (&x)[NDB], float sc, bool valid, int l32, int h32,
+                                    float* __restrict__ dst) {
+  constexpr int NV = 16 * NDB;
+  float v[NV];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[16 * db + r] = valid ? x[db][r] * sc : 0.f;
+  wave_colsum_vals<NV>(v, l32);
 #pragma unroll
   for (int j = 0; j < NV / 32; ++j) {
     const int idx = l32 * (NV / 32) + j, db = idx >> 4, r = idx & 15;
@@ -666,22 +674,6 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq4_kernel(AttnParams p) {
   const bf16_t* Kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* Vb = p.v + b * p.v_sb + hk * p.v_sh;
 
-  // Q and dO fragments of this wave's 32 queries (B operands of S^T = K Q^T, dP^T = V dO^T)
-  bf16x8 qf[D / 16], df[D / 16];
-  float L, dl;
-  {
-    const int qr = min(myq, p.T - 1);
-    const bf16_t* Qr = p.q + b * p.q_sb + hq * p.q_sh + (long)qr * p.q_st;
-    const bf16_t* Dr = p.dout + b * p.do_sb + hq * p.do_sh + (long)qr * p.do_st;
-#pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      qf[ks] = *reinterpret_cast<const bf16x8*>(Qr + ks * 16 + 8 * h32);
-      df[ks] = *reinterpret_cast<const bf16x8*>(Dr + ks * 16 + 8 * h32);
-    }
-    const long r = ((long)b * p.Hq + hq) * p.T + qr;
-    L = p.lse[r];
-    dl = p.delta[r];
-  }
   const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
   const int ntiles = (kend + BN - 1) / BN;
 
@@ -735,6 +727,53 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq4_kernel(AttnParams p) {
   f32x16 dq[NDB];
 #pragma unroll
   for (int db = 0; db < NDB; ++db) dq[db] = zero16();
+
+  // Prologue: the first K / V tile's DMA, then this wave's 32 query rows of Q, dO and O.
+  // delta = rowsum(dO O) is computed here (the one kernel that owns each query row) and
+  // written for the dK/dV kernel, which runs after this one -- no separate delta pass.  BIAS:
+  // also the QKV bias gradient's K and V columns of this 32-token block (attn_delta_kernel's
+  // identities: K columns 0, V columns the block's column sum of dO).
+  if (ntiles > 0) dma(0, std::integral_constant<int, 0>{});
+  bf16x8 qf[D / 16], df[D / 16];
+  float L, dl;
+  {
+    const int qr = min(myq, p.T - 1);
+    const bf16_t* Qr = p.q + b * p.q_sb + hq * p.q_sh + (long)qr * p.q_st;
+    const bf16_t* Dr = p.dout + b * p.do_sb + hq * p.do_sh + (long)qr * p.do_st;
+    const bf16_t* Or = p.o + b * p.o_sb + hq * p.o_sh + (long)qr * p.o_st;
+    bf16x8 of[D / 16];
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Qr + ks * 16 + 8 * h32);
+      df[ks] = *reinterpret_cast<const bf16x8*>(Dr + ks * 16 + 8 * h32);
+      of[ks] = *reinterpret_cast<const bf16x8*>(Or + ks * 16 + 8 * h32);
+    }
+    const long r = ((long)b * p.Hq + hq) * p.T + qr;
+    L = p.lse[r];
+    float d4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d4[j & 3] = fmaf(bf2f(of[ks][j]), bf2f(df[ks][j]), d4[j & 3]);
+    dl = (d4[0] + d4[1]) + (d4[2] + d4[3]);
+    dl += __shfl_xor(dl, 32);  // the other d half of the row
+    if (h32 == 0 && myq < p.T) const_cast<float*>(p.delta)[r] = dl;  // the scratch the dK/dV kernel reads
+    if constexpr (BIAS) {
+      if (qw0 < p.T) {  // T % 32 == 0: the wave's rows are one 32-token block
+        float* prow = p.bias_part + ((long)b * (p.T / 32) + qw0 / 32) * p.bias_ld + (long)(p.Hq + hq) * D;
+        float v[32];
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[8 * ks + j] = bf2f(df[ks][j]);
+        wave_colsum_vals<32>(v, l32);
+        // value index idx = l32 + ... -> column ks 16 + 8 h32 + j of idx = 8 ks + j
+        const int d = (l32 >> 3) * 16 + 8 * h32 + (l32 & 7);
+        prow[d] = 0.f;                    // K columns
+        prow[(long)p.Hkv * D + d] = v[0];  // V columns
+      }
+    }
+  }
 
   // one 32-key block (kb) of the tile in buffer BUF
   auto block = [&](int t, auto bufc, auto kbc) {
@@ -815,7 +854,6 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq4_kernel(AttnParams p) {
     block(t, bufc, std::integral_constant<int, 1>{});
   };
 
-  if (ntiles > 0) dma(0, std::integral_constant<int, 0>{});
   for (int t = 0; t < ntiles; t += 2) {
     tile(t, std::integral_constant<int, 0>{});
     if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
@@ -879,9 +917,6 @@ static void dq4_launch(const AttnParams& q, int grid, hipStream_t st) {
 
 template <int D, bool CAUSAL, bool BIAS = false>
 static void dq_launch(const AttnParams& q, int grid, hipStream_t st) {
-  if constexpr (D == 64) {
-    if (!dq_v3()) return dq4_launch<CAUSAL, BIAS>(q, grid, st);
-  }
   static bool done = false;
   if (!done) {
     (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, BIAS>,
@@ -922,14 +957,38 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
     }
     return (int)hipGetLastError();
   }
+  // D = 64 (attn_bwd_dq4): the dQ kernel first -- it computes delta (and, with the QKV bias,
+  // the K / V bias columns) in its prologue -- then dK/dV, which reads delta.  Otherwise (and
+  // with ORION_ATTN_DQ=v3): the delta pass, dK/dV, dQ.
+  const bool dq4 = D == 64 && !dq_v3();
   if (p.bias_part) {  // packed self-attention with the QKV bias gradient (GPT-2: D = 64, MHA)
     if (D != 64 || p.T != p.Tk || p.Hq != p.Hkv || p.T % 32) return -3;
+    if (dq4) {
+      if (causal) {
+        dq4_launch<true, true>(q, dq_grid, st);
+        kv_launch<64, true>(q, kv_grid, st);
+      } else {
+        dq4_launch<false, true>(q, dq_grid, st);
+        kv_launch<64, false>(q, kv_grid, st);
+      }
+      return (int)hipGetLastError();
+    }
 #define SPLITB(CC)                                                                                  \
   attn_delta_kernel<64, true><<<pre_grid, 256, 0, st>>>(q, delta);                                  \
   kv_launch<64, CC>(q, kv_grid, st);                                                                \
   dq_launch<64, CC, true>(q, dq_grid, st);
     if (causal) { SPLITB(true) } else { SPLITB(false) }
 #undef SPLITB
+    return (int)hipGetLastError();
+  }
+  if (dq4) {
+    if (causal) {
+      dq4_launch<true, false>(q, dq_grid, st);
+      kv_launch<64, true>(q, kv_grid, st);
+    } else {
+      dq4_launch<false, false>(q, dq_grid, st);
+      kv_launch<64, false>(q, kv_grid, st);
+    }
     return (int)hipGetLastError();
   }
 #define SPLIT(DD, CC)                                    \

@@ -19,7 +19,7 @@ struct AttnParams {
   // backward
   const unsigned short* dout;
   long do_sb, do_st, do_sh;
-  const float* delta;  // [B][Hq][T] = rowsum(dO * O)
+  const float* delta;  // [B][Hq][T] = rowsum(dO * O) (written by attn_bwd_dq4_kernel at D = 64)
   float* dq_acc;       // [B][Hq][T][D] fp32
   unsigned short* dk;
   long dk_sb, dk_st, dk_sh;
