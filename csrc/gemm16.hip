@@ -431,7 +431,9 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       r += __shfl_xor(r, 16);
       r += __shfl_xor(r, 32);
       const int m = mw + 16 * b + i16;
-      if (q == 0 && m < g.M) g.rowpart[(long)m * g.npart + nw / 128] = r;
+      // a wave whose 128 columns all lie past N (the last tile's second group when N % 256 <=
+      // 128, e.g. GPT-2's 50,304) has no partial: its index would be the next row's part 0
+      if (q == 0 && m < g.M && nw < g.N) g.rowpart[(long)m * g.npart + nw / 128] = r;
     }
   }
 }

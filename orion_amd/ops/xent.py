@@ -69,18 +69,22 @@ _LM_XT = os.environ.get("ORION_LMHEAD_XT", "1") == "1"
 _CREF = {}
 
 
-def _cref(dev):
-    """The running exp reference of the LM-head forward on ``dev`` (a device scalar the fold
-    kernel updates: the largest row log-sum-exp of the previous call).  Deterministic mode
+def _cref(dev, w=None):
+    """The running exp reference of the LM-head forward with weight ``w`` on ``dev`` (a device
+    scalar the fold kernel updates: the largest row log-sum-exp of the previous call), one per
+    weight tensor (keyed by its storage), so two models in one process -- a DDP trainer and its
+    local reference, say -- do not feed each other's forwards.  Deterministic mode
     (ops/determinism.py) uses a fresh 0 every call instead: the bf16 rounding of exp(logit -
     ref) depends on the reference, so a carried-over one would make two identical runs in one
-    process differ in the last bits (rows it does not suit take the exact fixup path)."""
+    process differ in the last bits (rows it does not suit take the exact fixup path).  Any
+    value is correct: the reference only decides which rows need the fixup."""
     from .determinism import deterministic
     if deterministic():
         return torch.zeros(1, dtype=torch.float32, device=dev)
-    t = _CREF.get(dev)
+    key = (dev, w.data_ptr() if w is not None else 0)
+    t = _CREF.get(key)
     if t is None:
-        t = _CREF[dev] = torch.zeros(1, dtype=torch.float32, device=dev)
+        t = _CREF[key] = torch.zeros(1, dtype=torch.float32, device=dev)
     return t
 
 
@@ -97,7 +101,7 @@ class _LinearXentExp(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, targets, ignore_index):
         t = targets.contiguous()
-        loss, e, invz, inv_n = C().lmhead_fwd(x, w, t, int(ignore_index), _cref(x.device))
+        loss, e, invz, inv_n = C().lmhead_fwd(x, w, t, int(ignore_index), _cref(x.device, w))
         ctx.save_for_backward(x, w, t, e, invz, inv_n)
         ctx.ignore = int(ignore_index)
         ctx.sink = sink_of(w)

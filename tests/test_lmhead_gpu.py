@@ -9,6 +9,7 @@ import torch
 import torch.nn.functional as F
 
 from orion_amd import ops
+from orion_amd.ops._ext import C
 from orion_amd.ops import xent as X
 from tolerance import check_all, rel_err, torch_bf16
 
@@ -54,7 +55,7 @@ def test_lmhead_exp_matches_fp32(N, spread):
     V, C = 50304, 768
     x, w, t = _case(N, V, C, spread)
     assert X.lmhead_exp_eligible(x, w)
-    X._cref(x.device).zero_()
+    X._cref(x.device, w).zero_()
     got = _run(x, w, t, 3.0)
     want = _ref(x, w, t, 3.0)
     lb, gb = torch_bf16(lambda a, b_: F.cross_entropy(a @ b_.t(), t, ignore_index=-1) * 3.0, (x, w),
@@ -65,13 +66,30 @@ def test_lmhead_exp_matches_fp32(N, spread):
     assert torch.count_nonzero(got[1][::7]) == 0
 
 
+@pytest.mark.parametrize("V", [50304, 32000, 1152])
+def test_lmhead_row_sums_every_column_once(V):
+    """Z_m (returned as 1 / Z) against the fp32 sum of exp(l - C) over exactly the V columns,
+    row by row: a wave past the last column (V % 256 <= 128: GPT-2's 50,304) once wrote a
+    zero partial into the next row's first slot (a race that dropped 128 columns from some
+    rows' Z, run to run); a dropped or doubled 128-column group moves Z by >= 1 / 400."""
+    C_, N = 768, 2048
+    x, w, t = _case(N, V, C_, False, seed=13)
+    cref = torch.zeros(1, device=DEV)
+    for _ in range(3):
+        cref.zero_()
+        loss, e, invz, inv_n = C().lmhead_fwd(x.detach(), w.detach(), t, -1, cref)
+        logits = x.detach().float() @ w.detach().float().t()
+        z = torch.exp(logits).sum(1)
+        assert ((1.0 / invz) / z - 1).abs().max() < 1e-3
+
+
 def test_lmhead_exp_vs_rowpass_forms():
     """The exp-epilogue form is at least as accurate against fp32 as the round-4 row pass
     (ORION_LMHEAD=rowpass: hipBLASLt logits + csrc/xent.hip) on the same large-spread inputs
     (near-one-hot rows make the two bf16 forms differ by a few percent from each other)."""
     V, C, N = 50304, 768, 1056
     x, w, t = _case(N, V, C, True, seed=3)
-    X._cref(x.device).zero_()
+    X._cref(x.device, w).zero_()
     a = _run(x, w, t, 1.0)
     old = X._LMHEAD
     X._LMHEAD = "rowpass"
@@ -97,7 +115,7 @@ def test_lmhead_transposed_wgrad_operand_is_bitwise_equal():
     try:
         for xt in (True, False):
             X._LM_XT = xt
-            X._cref(x.device).zero_()
+            X._cref(x.device, w).zero_()
             res.append(_run(x, w, t, 1.0))
     finally:
         X._LM_XT = old
@@ -111,7 +129,7 @@ def test_lmhead_fixup_every_row_and_reference_update():
     budget.  The reference then becomes the largest row log-sum-exp."""
     V, C, N = 50304, 768, 256
     x, w, t = _case(N, V, C, False, seed=5)
-    cref = X._cref(x.device)
+    cref = X._cref(x.device, w)
     cref.fill_(1.0e4)
     got = _run(x, w, t, 1.0)
     want = _ref(x, w, t, 1.0)
@@ -134,7 +152,7 @@ def test_lmhead_exp_llama_vocab_bwd_order():
     try:
         for first in (True, False):
             X._LM_WGRAD_FIRST = first
-            X._cref(x.device).zero_()
+            X._cref(x.device, w).zero_()
             got = _run(x, w, t, 2.0)
             check_all(("loss", "dx", "dw"), (got[0].reshape(1), got[1], got[2]),
                       (want[0].reshape(1), want[1], want[2]), ((lb / 2.0).detach().reshape(1), *gb))
