@@ -28,15 +28,14 @@ constexpr float LM_ZMIN = 7.888609052210118e-31f, LM_ZMAX = 1.2676506002282294e3
 
 ORION_DEVICE bool lm_valid(long t, long ignore, int V) { return t != ignore && t >= 0 && t < V; }
 
-// One wave per row: Z, lse, loss, the one-hot fold; rows to recompute go to fix_list.
+// One wave per row: Z, lse, loss, the one-hot fold; rows to recompute go to fix_list.  (The
+// valid-row count is the finalize kernel's: one global atomic per workgroup here -- 16,384 of
+// them on one address at GPT-2's shape -- serialised the kernel to ~0.19 ms.)
 __global__ __launch_bounds__(256) void lmhead_fold_kernel(
     const float* __restrict__ part, int npart, const float* __restrict__ tlog,
     const int64_t* __restrict__ tgt, long ignore, const float* __restrict__ cref, bf16_t* E,
     long lde, int V, int N, float* __restrict__ invz, float* __restrict__ lse,
     float* __restrict__ loss, int* __restrict__ counts, int* __restrict__ fix_list) {
-  __shared__ int nvalid;
-  if (threadIdx.x == 0) nvalid = 0;
-  __syncthreads();
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row < N) {
@@ -59,7 +58,6 @@ __global__ __launch_bounds__(256) void lmhead_fold_kernel(
     const float c = *cref;
     const bool fix = !(z >= LM_ZMIN && z <= LM_ZMAX);  // NaN / inf / 0 too
     if (lane == 0) {
-      if (valid) atomicAdd(&nvalid, 1);
       if (fix) {
         fix_list[atomicAdd(&counts[1], 1)] = (int)row;
       } else {
@@ -75,8 +73,6 @@ __global__ __launch_bounds__(256) void lmhead_fold_kernel(
       }
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0 && nvalid) atomicAdd(&counts[0], nvalid);
 }
 
 // Rows flagged by the fold: logits recomputed as a GEMV against W (two passes: the row max,
@@ -134,20 +130,22 @@ __global__ __launch_bounds__(256) void lmhead_fixup_kernel(
 // largest finite row lse (keeps every row's exp at most ~1 for the next weights).
 __global__ __launch_bounds__(1024) void lmhead_finalize_kernel(const float* __restrict__ loss_rows,
                                                                const float* __restrict__ lse, long N,
-                                                               const int* __restrict__ counts,
-                                                               float* __restrict__ out, float* __restrict__ inv_n,
-                                                               float* __restrict__ cref) {
+                                                               const int64_t* __restrict__ tgt, long ignore,
+                                                               int V, float* __restrict__ out,
+                                                               float* __restrict__ inv_n, float* __restrict__ cref) {
   __shared__ float red[16];
-  float s = 0.f, mx = -INFINITY;
+  float s = 0.f, mx = -INFINITY, nv = 0.f;
   for (long i = threadIdx.x; i < N; i += 1024) {
     s += loss_rows[i];
     const float l = lse[i];
     if (l == l && l < INFINITY) mx = fmaxf(mx, l);
+    nv += lm_valid(tgt[i], ignore, V) ? 1.f : 0.f;
   }
   s = block_sum<16>(s, red);
   mx = block_max<16>(mx, red);
+  nv = block_sum<16>(nv, red);  // exact: integer counts below 2^24 per lane sum
   if (threadIdx.x == 0) {
-    const float in = 1.f / fmaxf((float)counts[0], 1.f);
+    const float in = 1.f / fmaxf(nv, 1.f);
     inv_n[0] = in;
     out[0] = s * in;
     if (mx > -INFINITY) cref[0] = mx;
@@ -230,7 +228,7 @@ int orion_lmhead_fold(const float* part, int npart, const float* tlog, const int
   lmhead_fixup_kernel<<<64, 256, Cdim * sizeof(float), st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw,
                                                              Cdim, V, tlog, tgt, ignore, (bf16_t*)E, lde,
                                                              invz, lse, loss_rows, counts, fix_list);
-  lmhead_finalize_kernel<<<1, 1024, 0, st>>>(loss_rows, lse, N, counts, loss_out, inv_n, cref);
+  lmhead_finalize_kernel<<<1, 1024, 0, st>>>(loss_rows, lse, N, tgt, ignore, V, loss_out, inv_n, cref);
   return (int)hipGetLastError();
 }
 
