@@ -594,9 +594,12 @@ int64_t gemm_diag(int64_t flags) { return orion_gemm_set_diag((int)flags); }
 // out (..., N) = x (..., K) . op(w) with op(w) = w^T for w (N, K) [w_kmajor = false, the
 // nn.Linear forward] or w for w (K, N) [w_kmajor = true, the input gradient], and a fused
 // epilogue: 0 store, 1 + bias, 2 + bias then GELU (returns (a, gelu(a))), 3 times
-// GELU'(pre).  Returns (out, out2); out2 is undefined unless epi == 2.
-std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor, int64_t epi,
+// GELU'(pre); 2 | 0x100 returns (GELU'(a), gelu(a)) (the derivative for gemm_gelu_bwd's
+// pre_is_deriv form).  Returns (out, out2); out2 is undefined unless epi is 2.
+std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor, int64_t epi_in,
                                 const c10::optional<Tensor>& bias, const c10::optional<Tensor>& pre) {
+  TORCH_CHECK(epi_in == 0x102 || (epi_in >= 0 && epi_in <= 3), "gemm: unknown epilogue ", epi_in);
+  const int64_t epi = epi_in & 0xFF;
   check_bf16(x, "x");
   check_bf16(w, "w");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemm: w must be a contiguous 2-D tensor");
@@ -635,7 +638,7 @@ std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor,
     ldp = pc.stride(0);
   }
   check_launch(orion_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), (int)M, (int)N,
-                          (int)K, w_kmajor ? 1 : 0, (int)epi, out.data_ptr(), N, bp,
+                          (int)K, w_kmajor ? 1 : 0, (int)epi_in, out.data_ptr(), N, bp,
                           out2.defined() ? out2.data_ptr() : nullptr, N, pp, ldp, cur_stream()),
                "gemm");
   return {out, out2};
@@ -647,7 +650,7 @@ std::tuple<Tensor, Tensor> gemm(const Tensor& x, const Tensor& w, bool w_kmajor,
 // column-sum partials.  db goes into db_out (an fp32/bf16 gradient-arena slice) when given.
 std::tuple<Tensor, Tensor> gemm_gelu_bwd(const Tensor& dy, const Tensor& w, const Tensor& pre,
                                          const c10::optional<Tensor>& bias,
-                                         const c10::optional<Tensor>& db_out) {
+                                         const c10::optional<Tensor>& db_out, bool pre_is_deriv) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   check_bf16(pre, "pre");
@@ -675,8 +678,9 @@ std::tuple<Tensor, Tensor> gemm_gelu_bwd(const Tensor& dy, const Tensor& w, cons
   auto db = given ? *db_out : at::empty({N}, bias.has_value() && bias->defined() ? bias->options() : dy.options());
   auto part = at::empty({(long)orion_gemm_colsum_scratch((int)M, (int)N)}, dy.options().dtype(at::kFloat));
   check_launch(orion_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), (int)M, (int)N,
-                          (int)K, 1, 3, out.data_ptr(), N, bp, nullptr, 0, pc.data_ptr(), pc.stride(0),
-                          cur_stream(), db.data_ptr(), is_f32(db) ? 1 : 0, part.data_ptr<float>()),
+                          (int)K, 1, 3 | (pre_is_deriv ? 0x100 : 0), out.data_ptr(), N, bp, nullptr, 0,
+                          pc.data_ptr(), pc.stride(0), cur_stream(), db.data_ptr(), is_f32(db) ? 1 : 0,
+                          part.data_ptr<float>()),
                "gemm_gelu_bwd");
   return {out.view(sizes), given ? Tensor() : db};
 }
@@ -1039,7 +1043,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("lmhead_bwd_prep(Tensor x, Tensor targets, int ignore_index, int V, Tensor invz, Tensor inv_n, Tensor g, bool transposed=False) -> (Tensor, Tensor)");
   m.def("gemm_rowscale(Tensor e, Tensor w, Tensor srow) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
-  m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None) -> (Tensor, Tensor)");
+  m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None, bool pre_is_deriv=False) -> (Tensor, Tensor)");
   m.def("gemm_swiglu_bwd(Tensor dy, Tensor w, Tensor gate_up) -> Tensor");
   m.def("grad_sumsq(Tensor g, Tensor(a!) out) -> ()");
   m.def("adamw_flat(Tensor(a!) p16, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor g, Tensor decay, Tensor hyper, Tensor sumsq) -> ()");

@@ -147,6 +147,12 @@ ORION_DEVICE f32x2 sigmoid2u_x2(f32x2 x, f32x2 x2) {
   return f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 ORION_DEVICE f32x2 gelu_x2(f32x2 x) { return x * sigmoid2u_x2(x, x * x); }
+// gelu(x) and GELU'(x) on one sigmoid
+ORION_DEVICE void gelu_and_grad_x2(f32x2 x, f32x2& g, f32x2& d) {
+  const f32x2 x2 = x * x, s = sigmoid2u_x2(x, x2);
+  g = x * s;
+  d = fma2(fma2(-s, s, s), x * fma2(x2, splat2(GELU_D), splat2(GELU_C)), s);
+}
 ORION_DEVICE f32x2 gelu_grad_x2(f32x2 x) {
   const f32x2 x2 = x * x, s = sigmoid2u_x2(x, x2);
   return fma2(fma2(-s, s, s), x * fma2(x2, splat2(GELU_D), splat2(GELU_C)), s);

@@ -64,6 +64,11 @@ int orion_gemm_colsum_scratch(int M, int N) { return ((M + 63) / 64 + 32) * N; }
 int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, int wkm,
                int epi, void* out, long ldo, const void* bias, void* out2, long ldo2,
                const void* pre, long ldp, hipStream_t st, void* db, int db_f32, float* part) {
+  // epi | GEMM_DERIV: the GELU derivative form (GemmArgs::deriv) of EPI_BIAS_GELU / EPI_GELU_BWD
+  const int deriv = (epi & GEMM_DERIV) ? 1 : 0;
+  epi &= ~GEMM_DERIV;
+  if (deriv && epi != EPI_BIAS_GELU && epi != EPI_GELU_BWD) return -3;
+  if (deriv && epi == EPI_GELU_BWD && bias) return -3;  // the bias is inside the stored derivative
   if (M < 1 || K < 64 || K % 64 || N % 8 || N < 8) return -1;
   if ((ldx | ldw | ldo) % 8) return -1;
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
@@ -77,6 +82,7 @@ int orion_gemm(const void* X, long ldx, const void* W, long ldw, int M, int N, i
   GemmArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)out, ldo,
              (const bf16_t*)bias, (bf16_t*)out2, ldo2, (const bf16_t*)pre, ldp,
              M, N, K, (N + 255) / 256, gemm_diag()};
+  a.deriv = deriv;
   if ((a.flags & 4) && epi <= EPI_BIAS_GELU) a.slabs = (float*)pre;  // slot stamps (diagnostic)
   if (!gemm16_ok(a, wkm)) return -1;
   const int rows = (M + 63) / 64;

@@ -288,7 +288,10 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       }
       if constexpr (EPI == EPI_GELU_BWD) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] *= G16_DIAG_GELU ? gelu_grad_x2(unpack2(p4[e]) + bias[e]) : unpack2(p4[e]) + bias[e];
+        for (int e = 0; e < 4; ++e) {
+          if (g.deriv) v[e] *= unpack2(p4[e]);  // pre holds GELU'(a) (bias already inside)
+          else v[e] *= G16_DIAG_GELU ? gelu_grad_x2(unpack2(p4[e]) + bias[e]) : unpack2(p4[e]) + bias[e];
+        }
       }
       if constexpr (EPI == EPI_EXP) {
         // the target's logit (fp32, before the exp) for the loss; exp(acc - cref) and its row sum
@@ -325,13 +328,23 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
         }
       }
       u32x4 pk, pk2;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(v[e]);
-      if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
+      if (EPI == EPI_BIAS_GELU && G16_DIAG_GELU && g.deriv) {  // (GELU'(a), gelu(a))
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if constexpr (EPI == EPI_BIAS_GELU) pk2[e] = pack2_bf16(G16_DIAG_GELU ? gelu_x2(v[e]) : v[e] * v[e]);
-          else pk2[e] = pack2_bf16(du[e]);
+          f32x2 ge, de;
+          gelu_and_grad_x2(v[e], ge, de);
+          pk[e] = pack2_bf16(de);
+          pk2[e] = pack2_bf16(ge);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(v[e]);
+        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if constexpr (EPI == EPI_BIAS_GELU) pk2[e] = pack2_bf16(G16_DIAG_GELU ? gelu_x2(v[e]) : v[e] * v[e]);
+            else pk2[e] = pack2_bf16(du[e]);
+          }
         }
       }
       // bias + GELU: the pre-activation is read again only by the backward -- streamed past

@@ -8,6 +8,7 @@ namespace orion {
 
 enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3, EPI_WGRAD = 4,
                EPI_SWIGLU_BWD = 5, EPI_EXP = 6, EPI_ROWSCALE = 7 };
+constexpr int GEMM_DERIV = 0x100;  // orion_gemm's epi flag: GemmArgs::deriv
 
 struct GemmArgs {
   const bf16_t* X;  long ldx;   // [M][K] row-major
@@ -38,6 +39,9 @@ struct GemmArgs {
   float* tlog;
   const float* cref;
   const float* rs;
+  // GELU derivative stored instead of the pre-activation (GPT-2 MLP, round 5): EPI_BIAS_GELU
+  // writes GELU'(a) as its first output, EPI_GELU_BWD multiplies by pre as given
+  int deriv;
 };
 
 // ---- 16x16x32 kernel helpers (csrc/gemm16.hip)

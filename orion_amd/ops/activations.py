@@ -156,9 +156,13 @@ class _FusedMLP(torch.autograd.Function):
         C_ = x.shape[-1]
         x2 = x.reshape(-1, C_)
         bb = None if b_fc is None else b_fc.to(torch.bfloat16)
+        ctx.deriv = False
         if bb is None:
             a = linear_fwd(x2, w_fc)
             h = C().bias_gelu_fwd(a, None).view(a.shape)
+        elif _GELU_DERIV:  # a = GELU'(x W_fc^T + b_fc): the backward epilogue only multiplies
+            a, h = C().gemm(x2, w_fc, False, EPI_BIAS_GELU | GEMM_DERIV, bb, None)
+            ctx.deriv = True
         else:
             a, h = C().gemm(x2, w_fc, False, EPI_BIAS_GELU, bb, None)
         y = linear_fwd(h, w_proj, b_proj)
@@ -175,8 +179,8 @@ class _FusedMLP(torch.autograd.Function):
         s_fc, s_proj = ctx.sinks
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         sbfc, sbproj = _claim((b_fc, b_proj))
-        # a already holds the fc bias: GELU'(a), no bias operand
-        da, dbfc = C().gemm_gelu_bwd(dy2, w_proj, a, None, _view(sbfc))
+        # a already holds the fc bias: GELU'(a), no bias operand (or a IS the derivative)
+        da, dbfc = C().gemm_gelu_bwd(dy2, w_proj, a, None, _view(sbfc), ctx.deriv)
         _notify(sbfc)
         dbfc = None if b_fc is None else _unless(dbfc, sbfc)
         grads = [None, None, None, None, None]
@@ -210,6 +214,13 @@ class _FusedMLP(torch.autograd.Function):
         if dbfc is not None:
             grads[2] = dbfc.to(b_fc.dtype)
         return tuple(grads)
+
+
+# ORION_GELU_DERIV=1 (default, round 5): the fused MLP's forward epilogue stores GELU'(a) in
+# place of the pre-activation a (one sigmoid for gelu and GELU'), so the backward epilogue
+# multiplies instead of evaluating GELU' (exp + rcp per element) in the store-bound GEMM.
+_GELU_DERIV = os.environ.get("ORION_GELU_DERIV", "1") == "1"
+GEMM_DERIV = 0x100
 
 
 # Order of the MLP backward's GEMMs after the fused GELU' one: 1 (default) = the fc input and

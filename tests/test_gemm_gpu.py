@@ -80,6 +80,29 @@ def test_gemm_gelu_backward_epilogue(M, N, K, gemm_cfg):
     within_bf16_budget("da", out, want, (dy @ w) * _gelu_grad(pre.float()).bfloat16())
 
 
+@pytest.mark.parametrize("M,N,K", SHAPES[:6])
+def test_gemm_gelu_derivative_forms(M, N, K, gemm_cfg):
+    """The derivative form of the fused MLP (ORION_GELU_DERIV): the forward epilogue returns
+    (GELU'(a), gelu(a)) for a = x w^T + b (epi 2 | 0x100), and gemm_gelu_bwd with
+    pre_is_deriv multiplies by that stored derivative -- against fp32, and the backward equal
+    to the pre-activation form within the bf16 budget."""
+    g = torch.Generator(device=DEV).manual_seed(13 + M + N)
+    x, w, b = _rnd(g, M, K), _rnd(g, N, K), _rnd(g, N)
+    a = x.float() @ w.float().t() + b.float()
+    ab = torch.nn.functional.linear(x, w, b)
+    d, h = _C().gemm(x, w, False, 0x102, b, None)
+    within_bf16_budget("gelu'", d, _gelu_grad(a), _gelu_grad(ab.float()).bfloat16())
+    within_bf16_budget("gelu", h, ref.gelu_tanh(a), torch.nn.functional.gelu(ab, approximate="tanh"))
+    dy, w2 = _rnd(g, M, 384), _rnd(g, 384, N)
+    da, db = _C().gemm_gelu_bwd(dy, w2, d, None, None, True)
+    want = (dy.float() @ w2.float()) * _gelu_grad(a)
+    base = (dy @ w2) * _gelu_grad(ab.float()).bfloat16()
+    within_bf16_budget("da", da, want, base)
+    within_bf16_budget("db", db, want.sum(0), base.float().sum(0).bfloat16())
+    with pytest.raises(RuntimeError):  # the bias is inside the stored derivative
+        _C().gemm_gelu_bwd(dy, w2, d, b, None, True)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 768, 768), (4096, 3072, 768), (777, 264, 128)])
 @pytest.mark.parametrize("arena", [None, torch.float32, torch.bfloat16])
 def test_gemm_gelu_bwd_with_bias_grad(M, N, K, arena, gemm_cfg):
