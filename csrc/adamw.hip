@@ -75,6 +75,10 @@ __global__ __launch_bounds__(1024) void sum_partials_kernel(const float* __restr
   if (threadIdx.x == 0) out[0] = s;
 }
 
+#ifndef ADAMW_UNROLL
+#define ADAMW_UNROLL 2
+#endif
+
 // hyper = [lr, beta1, beta2, eps, weight_decay, 1-beta1^t, 1-beta2^t, max_grad_norm]
 template <typename G>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(
@@ -90,28 +94,45 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
   }
   const float step = lr / bc1;
   const float inv_bc2 = 1.f / bc2;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    const long e = i * 4;
-    const float dec = decay[e / ADAM_CHUNK] ? (1.f - lr * wd) : 1.f;
-    f32x4 w = ld_stream(reinterpret_cast<const f32x4*>(master + e));
-    f32x4 mm = ld_stream(reinterpret_cast<const f32x4*>(m + e));
-    f32x4 vv = ld_stream(reinterpret_cast<const f32x4*>(v + e));
-    float gg[4];
-    load4(g, e, gg);
-    bf16x4 out;
+  // ADAMW_UNROLL groups of 4 elements per thread and iteration, every load of the iteration
+  // issued before the first update (more bytes in flight per thread; same per-element math)
+  const long stride = (long)gridDim.x * 256;
+  for (long i0 = blockIdx.x * 256L + threadIdx.x; i0 < n4; i0 += ADAMW_UNROLL * stride) {
+    f32x4 w[ADAMW_UNROLL], mm[ADAMW_UNROLL], vv[ADAMW_UNROLL];
+    float gg[ADAMW_UNROLL][4];
+    float dec[ADAMW_UNROLL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gr = gg[j] * cs;
-      mm[j] = b1 * mm[j] + (1.f - b1) * gr;
-      vv[j] = b2 * vv[j] + (1.f - b2) * gr * gr;
-      const float denom = sqrtf(vv[j] * inv_bc2) + eps;
-      w[j] = w[j] * dec - step * mm[j] / denom;
-      out[j] = f2bf(w[j]);
+    for (int u = 0; u < ADAMW_UNROLL; ++u) {
+      const long i = i0 + u * stride;
+      if (u == 0 || i < n4) {
+        const long e = i * 4;
+        dec[u] = decay[e / ADAM_CHUNK] ? (1.f - lr * wd) : 1.f;
+        w[u] = ld_stream(reinterpret_cast<const f32x4*>(master + e));
+        mm[u] = ld_stream(reinterpret_cast<const f32x4*>(m + e));
+        vv[u] = ld_stream(reinterpret_cast<const f32x4*>(v + e));
+        load4(g, e, gg[u]);
+      }
     }
-    st_stream(w, reinterpret_cast<f32x4*>(master + e));
-    st_stream(mm, reinterpret_cast<f32x4*>(m + e));
-    st_stream(vv, reinterpret_cast<f32x4*>(v + e));
-    st_stream(out, reinterpret_cast<bf16x4*>(p16 + e));
+#pragma unroll
+    for (int u = 0; u < ADAMW_UNROLL; ++u) {
+      const long i = i0 + u * stride;
+      if (u > 0 && i >= n4) break;
+      const long e = i * 4;
+      bf16x4 out;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gr = gg[u][j] * cs;
+        mm[u][j] = b1 * mm[u][j] + (1.f - b1) * gr;
+        vv[u][j] = b2 * vv[u][j] + (1.f - b2) * gr * gr;
+        const float denom = sqrtf(vv[u][j] * inv_bc2) + eps;
+        w[u][j] = w[u][j] * dec[u] - step * mm[u][j] / denom;
+        out[j] = f2bf(w[u][j]);
+      }
+      st_stream(w[u], reinterpret_cast<f32x4*>(master + e));
+      st_stream(mm[u], reinterpret_cast<f32x4*>(m + e));
+      st_stream(vv[u], reinterpret_cast<f32x4*>(v + e));
+      st_stream(out, reinterpret_cast<bf16x4*>(p16 + e));
+    }
   }
 }
 
