@@ -174,7 +174,8 @@ def test_bench_spawns_its_own_ranks_on_cpu(zero1):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
     assert rec["steps"] == 2 and rec["warmup"] == 1
-    assert abs(rec["per_gpu"] * 2 - rec["value"]) / rec["value"] < 1e-3
+    # both rounded to 0.1 tok/s: at CPU rates (tens of tok/s) that alone is ~1e-3 relative
+    assert abs(rec["per_gpu"] * 2 - rec["value"]) <= 0.1 * 2 + 1e-3 * rec["value"]
     assert rec["allreduce_busbw_gbps"] is not None
     # bucket timeline of the last step: every bucket ready before it completed
     ddp = rec["ddp_buckets"]
