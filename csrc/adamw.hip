@@ -6,6 +6,7 @@
 // and the global gradient sum-of-squares are read from DEVICE memory, so a
 // captured HIP graph replays correct steps without host round trips.
 // 26 bytes/element of HBM traffic: the 124M-parameter step is ~3.2 GB, ~0.6 ms.
+#include <cstdlib>
 #include "common.h"
 
 // non-temporal loads / stores for the once-per-step streams (A/B builds: -DADAMW_NT=0/1)
@@ -158,8 +159,17 @@ int orion_adamw_flat(void* p16, float* master, float* m, float* v, const void* g
                      hipStream_t st) {
   if (n % ADAM_CHUNK) return -1;
   const long n4 = n / 4;
+  // One 4-element group per thread (the loop only runs past 2^22 workgroups): on MI355X the
+  // one-shot grid streams at 5.8-6.1 TB/s over GPT-2's arena against 4.4-4.6 for a 4,096-
+  // workgroup grid-stride loop (0.61-0.64 vs 0.82-0.86 ms; 1 G parameters 5.03 vs 5.68 ms;
+  // profiles/ab/adamw_grid_r05.log).  ORION_ADAMW_GRID (diagnostic) caps the grid.
+  static const long cap = [] {
+    const char* e = getenv("ORION_ADAMW_GRID");
+    const long c = e ? atol(e) : 0;
+    return c > 0 ? c : (1L << 22);
+  }();
   long grid = (n4 + 255) / 256;
-  if (grid > 4096) grid = 4096;
+  if (grid > cap) grid = cap;
   if (g_f32)
     adamw_flat_kernel<float><<<(int)grid, 256, 0, st>>>((bf16_t*)p16, master, m, v, (const float*)g,
                                                         decay, hyper, sumsq, n4);
