@@ -84,6 +84,8 @@ def _cref(dev, w=None):
     key = (dev, w.data_ptr() if w is not None else 0)
     t = _CREF.get(key)
     if t is None:
+        if len(_CREF) >= 64:  # freed weights' storages are reused: keep the table bounded
+            _CREF.clear()
         t = _CREF[key] = torch.zeros(1, dtype=torch.float32, device=dev)
     return t
 
