@@ -122,11 +122,14 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(
       bf16x4 out;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        // every multiply-add an explicit fmaf: left to the compiler's contraction, the two
+        // unrolled copies fused differently (1-ulp differences between elements handled by
+        // slot 0 and slot 1, i.e. results depending on the grid: tests/test_grid_forms_gpu.py)
         const float gr = gg[u][j] * cs;
-        mm[u][j] = b1 * mm[u][j] + (1.f - b1) * gr;
-        vv[u][j] = b2 * vv[u][j] + (1.f - b2) * gr * gr;
+        mm[u][j] = fmaf(b1, mm[u][j], (1.f - b1) * gr);
+        vv[u][j] = fmaf(b2, vv[u][j], ((1.f - b2) * gr) * gr);
         const float denom = sqrtf(vv[u][j] * inv_bc2) + eps;
-        w[u][j] = w[u][j] * dec[u] - step * mm[u][j] / denom;
+        w[u][j] = fmaf(w[u][j], dec[u], -(step * mm[u][j] / denom));
         out[j] = f2bf(w[u][j]);
       }
       st_stream(w[u], reinterpret_cast<f32x4*>(master + e));
