@@ -220,7 +220,7 @@ int orion_lmhead_fold(const float* part, int npart, const float* tlog, const int
                       float* cref, void* E, long lde, int V, long N, const void* X, long ldx, const void* W,
                       long ldw, int Cdim, float* invz, float* lse, float* loss_rows, int* counts,
                       int* fix_list, float* loss_out, float* inv_n, hipStream_t st) {
-  if (N <= 0 || N > 0x7FFFFFFFL || Cdim % 8) return -1;
+  if (N <= 0 || N > 0x7FFFFFFFL || Cdim % 8 || Cdim > 16384) return -1;  // fixup LDS: Cdim floats
   if (hipMemsetAsync(counts, 0, 16, st) != hipSuccess) return -2;
   lmhead_fold_kernel<<<(unsigned)((N + 3) / 4), 256, 0, st>>>(part, npart, tlog, tgt, ignore, cref,
                                                               (bf16_t*)E, lde, V, (int)N, invz, lse,

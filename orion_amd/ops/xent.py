@@ -93,6 +93,7 @@ def _cref(dev, w=None):
 def lmhead_exp_eligible(x, w) -> bool:
     return (_LMHEAD == "exp" and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.dim() == 2 and x.stride(1) == 1 and w.is_contiguous() and x.shape[1] % 64 == 0
+            and x.shape[1] <= 16384
             and w.shape[0] % 64 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0
             and w.data_ptr() % 16 == 0 and x.shape[0] % 32 == 0)
 
