@@ -30,9 +30,25 @@ SHAPES = [("lmhead_fwd", 50304, 768, 0), ("fc_fwd_gelu", 3072, 768, 2), ("qkv_fw
           ("wgrad_qkv", 2304, 768, -1), ("wgrad_fc", 3072, 768, -1), ("wgrad_lmhead", 50304, 768, -1)]
 if a.backward:
     SHAPES = [s for s in SHAPES if "fwd" not in s[0]]
+SHAPES += [("lmhead_exp_fwd", 50304, 768, 6), ("lmhead_rowscale_dgrad", 768, 50304, 7)]
+if a.backward:
+    SHAPES = [s for s in SHAPES if "fwd" not in s[0]]
 for name, N, K, epi in SHAPES:
+    if epi == 6:  # LM head forward through the exp epilogue (+ the fold)
+        x, w = rnd(M, K), rnd(N, K) * 0.1
+        tg = torch.randint(0, N, (M,), device="cuda", generator=g)
+        cref = torch.zeros(1, device="cuda")
+        f = lambda: ops.lmhead_fwd(x, w, tg, -1, cref)  # noqa: E731
+        fl_mnk = (M, N, K)
+    elif epi == 7:  # LM head input gradient: row-scaled E W
+        x, w = rnd(M, K), rnd(K, N)
+        srow = torch.rand(M, device="cuda", generator=g)
+        f = lambda: ops.gemm_rowscale(x, w, srow)  # noqa: E731
+        fl_mnk = (M, N, K)
     kind_dgrad = name.endswith("dgrad") or (name.endswith("gelu") and epi == 3)
-    if epi == -1:  # weight gradient: dy (M x N) ^T x (M x K), k-major operands, split-K as chosen
+    if epi in (6, 7):
+        pass
+    elif epi == -1:  # weight gradient: dy (M x N) ^T x (M x K), k-major operands, split-K as chosen
         x, w = rnd(M, N), rnd(M, K)
         f = lambda: ops.wgrad(x, w, None, 0)  # noqa: E731
         fl_mnk = (N, K, M)
