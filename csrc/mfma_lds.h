@@ -178,9 +178,14 @@ ORION_DEVICE void lds_wait_frags(bf16x8 (&af)[TA], bf16x8 (&bf)[2]) {
 // SIMD the arbiter then feeds the matrix pipe first and the other waves' softmax / staging VALU
 // fills the gaps.  Measured: Llama-shape backward -1.5 %, forward -1.3 %, GPT-2 step faster in
 // 3 of 3 alternating pairs (profiles/ab/attn_setprio_r04.log).
+#ifndef ORION_MFMA_PRIO
+#define ORION_MFMA_PRIO 1  // wave priority while issuing MFMA blocks (0: off, A/B builds)
+#endif
 ORION_DEVICE void mfma_prio(bool on) {
-  if (on) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
+  if constexpr (ORION_MFMA_PRIO > 0) {
+    if (on) __builtin_amdgcn_s_setprio(ORION_MFMA_PRIO);
+    else __builtin_amdgcn_s_setprio(0);
+  }
 }
 
 template <int N>
