@@ -31,4 +31,5 @@ for _ in range(30):
     e1.synchronize()
     ts.append(e0.elapsed_time(e1))
 t = sorted(ts)[15]
-print(json.dumps({"ms": round(t, 4), "TBs": round(4 * R * Cn * 2 / t / 1e9, 2), "nb": os.environ.get("ORION_LN_BWD_NB", "default")}))
+nb = os.environ.get("ORION_LN_BWD_NB", "default")
+print(json.dumps({"ms": round(t, 4), "TBs": round(4 * R * Cn * 2 / t / 1e9, 2), "nb": nb}))
