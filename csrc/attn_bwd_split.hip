@@ -9,10 +9,11 @@
 // The split recomputes S and dP once more (7 instead of 5 matmuls per (q, key) pair) but
 // each kernel keeps its accumulators and operand fragments in registers:
 //
-//   delta          delta[q] = sum_d dO O: a separate HBM-bound pass (computing it inside the
-//                  dQ kernel measured 0.3 % slower end to end -- its extra O loads sit in the
-//                  prologue ahead of the first K/V tile -- and was removed in round 5;
-//                  profiles/ab/ab_attn_delta.log)
+//   delta          delta[q] = sum_d dO O.  D = 64 (the default attn_bwd_dq4 path): written by
+//                  the dQ kernel's prologue (with the QKV bias, also the K / V bias columns),
+//                  so dQ is launched FIRST and dK/dV, which reads delta, after it on the same
+//                  stream.  D = 128 and ORION_ATTN_DQ=v3: a separate HBM-bound pass
+//                  (attn_delta_kernel) ahead of both kernels.
 //   kv kernel      per workgroup 32*NW keys, loop over 32-row query tiles (and the query
 //                  heads of its KV head):  S = Q K^T, dP = dO V^T (key on the lane, V
 //                  fragments in registers, K in registers or an LDS image),
@@ -927,7 +928,9 @@ static void dq_launch(const AttnParams& q, int grid, hipStream_t st) {
 }
 
 // delta (caller-allocated [B][Hq][T] fp32 scratch), dK/dV and dQ; p.dq / dk / dv are bf16
-// outputs (strided views allowed).  Order: delta pass, dK/dV, dQ.
+// outputs (strided views allowed).  Order on stream st: D = 64 -- dQ (attn_bwd_dq4, writes
+// delta and the bias K / V columns), then dK/dV (reads delta); otherwise the delta pass, dK/dV,
+// dQ.
 int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
   // 32-bit buffer offsets: the dQ kernel addresses one (batch, KV head)'s K / V, the dK/dV
   // kernel one batch's Q / dO over all query heads; beyond 2 GB the caller takes the fused

@@ -39,7 +39,7 @@ int orion_wgrad_effective_splits(int, int);
 int orion_wgrad_tail_rows(int, int, int, int*);
 int orion_wgrad(const void*, long, const void*, long, int, int, int, int, float*, void*,
                 const float*, int, int, int, hipStream_t);
-int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, hipStream_t);
+int orion_xent_fwd_bwd(void*, const int64_t*, float*, float*, float*, long, int, long, int*, hipStream_t);
 int orion_sumsq_partials();
 int orion_grad_sumsq(const void*, long, int, float*, float*, hipStream_t);
 int orion_adamw_flat(void*, float*, float*, float*, const void*, int, const uint8_t*, const float*,
@@ -63,7 +63,7 @@ int orion_gemm_lm(const void*, long, const void*, long, int, int, int, int, void
                   const int64_t*, float*, const float*, const float*, hipStream_t);
 int orion_lmhead_fold(const float*, int, const float*, const int64_t*, long, float*, void*, long, int, long,
                       const void*, long, const void*, long, int, float*, float*, float*, int*, int*, float*,
-                      float*, hipStream_t);
+                      float*, int*, hipStream_t);
 int orion_lmhead_bwd_prep(const void*, long, int, long, const int64_t*, long, int, const float*, const float*,
                           const float*, float*, void*, int, hipStream_t);
 int orion_gemm_set_diag(int flags);
@@ -442,7 +442,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lmhead_fwd(const Tensor& x, const Ten
                                  x.stride(0), w.data_ptr(), w.stride(0), Cd, invz.data_ptr<float>(),
                                  lse.data_ptr<float>(), lrow.data_ptr<float>(), ints.data_ptr<int>(),
                                  ints.data_ptr<int>() + 4, loss.data_ptr<float>(), inv_n.data_ptr<float>(),
-                                 cur_stream()),
+                                 id_error_flag(x.device().index()), cur_stream()),
                "lmhead_fold");
   return {loss, E, invz, inv_n};
 }
@@ -500,7 +500,7 @@ Tensor xent_fwd_bwd(Tensor logits, const Tensor& targets, int64_t ignore_index) 
   auto loss = at::empty({}, fopts);
   check_launch(orion_xent_fwd_bwd(logits.data_ptr(), t.data_ptr<int64_t>(), losses.data_ptr<float>(),
                                   inv_n.data_ptr<float>(), loss.data_ptr<float>(), N, V,
-                                  ignore_index, cur_stream()),
+                                  ignore_index, id_error_flag(logits.device().index()), cur_stream()),
                "xent_fwd_bwd");
   return loss;
 }

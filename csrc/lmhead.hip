@@ -132,19 +132,24 @@ __global__ __launch_bounds__(1024) void lmhead_finalize_kernel(const float* __re
                                                                const float* __restrict__ lse, long N,
                                                                const int64_t* __restrict__ tgt, long ignore,
                                                                int V, float* __restrict__ out,
-                                                               float* __restrict__ inv_n, float* __restrict__ cref) {
+                                                               float* __restrict__ inv_n, float* __restrict__ cref,
+                                                               int* __restrict__ err) {
   __shared__ float red[16];
-  float s = 0.f, mx = -INFINITY, nv = 0.f;
+  float s = 0.f, mx = -INFINITY, nv = 0.f, bad = 0.f;
   for (long i = threadIdx.x; i < N; i += 1024) {
     s += loss_rows[i];
     const float l = lse[i];
     if (l == l && l < INFINITY) mx = fmaxf(mx, l);
-    nv += lm_valid(tgt[i], ignore, V) ? 1.f : 0.f;
+    const long t = tgt[i];
+    nv += lm_valid(t, ignore, V) ? 1.f : 0.f;
+    bad += (t != ignore && !lm_valid(t, ignore, V)) ? 1.f : 0.f;
   }
   s = block_sum<16>(s, red);
   mx = block_max<16>(mx, red);
   nv = block_sum<16>(nv, red);  // exact: integer counts below 2^24 per lane sum
+  bad = block_sum<16>(bad, red);
   if (threadIdx.x == 0) {
+    if (bad > 0.f) err[0] = 1;  // an out-of-range target (not ignore_index): skipped, flagged
     const float in = 1.f / fmaxf(nv, 1.f);
     inv_n[0] = in;
     out[0] = s * in;
@@ -219,7 +224,7 @@ using namespace orion;
 int orion_lmhead_fold(const float* part, int npart, const float* tlog, const int64_t* tgt, long ignore,
                       float* cref, void* E, long lde, int V, long N, const void* X, long ldx, const void* W,
                       long ldw, int Cdim, float* invz, float* lse, float* loss_rows, int* counts,
-                      int* fix_list, float* loss_out, float* inv_n, hipStream_t st) {
+                      int* fix_list, float* loss_out, float* inv_n, int* err, hipStream_t st) {
   if (N <= 0 || N > 0x7FFFFFFFL || Cdim % 8 || Cdim > 16384) return -1;  // fixup LDS: Cdim floats
   if (hipMemsetAsync(counts, 0, 16, st) != hipSuccess) return -2;
   lmhead_fold_kernel<<<(unsigned)((N + 3) / 4), 256, 0, st>>>(part, npart, tlog, tgt, ignore, cref,
@@ -228,7 +233,7 @@ int orion_lmhead_fold(const float* part, int npart, const float* tlog, const int
   lmhead_fixup_kernel<<<64, 256, Cdim * sizeof(float), st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw,
                                                              Cdim, V, tlog, tgt, ignore, (bf16_t*)E, lde,
                                                              invz, lse, loss_rows, counts, fix_list);
-  lmhead_finalize_kernel<<<1, 1024, 0, st>>>(loss_rows, lse, N, tgt, ignore, V, loss_out, inv_n, cref);
+  lmhead_finalize_kernel<<<1, 1024, 0, st>>>(loss_rows, lse, N, tgt, ignore, V, loss_out, inv_n, cref, err);
   return (int)hipGetLastError();
 }
 

@@ -23,28 +23,26 @@
 namespace orion {
 
 
-// inv_n[0] = 1 / max(1, #targets != ignore_index).  One workgroup; 8 independent
-// loads in flight per thread so the pass is bandwidth- not latency-bound (the
-// previous one-load-at-a-time loop took ~56 us for 32k targets).
-template <typename T>
-__device__ __forceinline__ float n_valid(T v, long ignore);
-template <>
-__device__ __forceinline__ float n_valid<i64x2>(i64x2 v, long ignore) {
-  return (v[0] != ignore ? 1.f : 0.f) + (v[1] != ignore ? 1.f : 0.f);
-}
-template <>
-__device__ __forceinline__ float n_valid<int64_t>(int64_t v, long ignore) {
-  return v != ignore ? 1.f : 0.f;
+// inv_n[0] = 1 / max(1, #valid targets).  A target is valid when it is not ignore_index and
+// lies in [0, V) (the same rule as csrc/lmhead.hip's lm_valid); any other target is skipped
+// (no loss, no gradient) and raises the device flag ``err`` (ops.embedding.id_error, where
+// torch's cross_entropy would raise).  One workgroup; 8 independent loads in flight per
+// thread so the pass is bandwidth- not latency-bound.
+__device__ __forceinline__ void tgt_count(long v, long ignore, int V, float& c, float& bad) {
+  const bool in = v >= 0 && v < V;
+  c += (v != ignore && in) ? 1.f : 0.f;
+  bad += (v != ignore && !in) ? 1.f : 0.f;
 }
 
 template <typename T>  // i64x2 when the targets are 16-byte aligned, else int64_t
 __global__ __launch_bounds__(1024) void count_valid_kernel(const int64_t* __restrict__ t, long N,
-                                                           long ignore, float* __restrict__ inv_n) {
+                                                           long ignore, int V, float* __restrict__ inv_n,
+                                                           int* __restrict__ err) {
   __shared__ float red[16];
   constexpr int PER = sizeof(T) / sizeof(int64_t);
   const long NV = N / PER;
   const T* tv = reinterpret_cast<const T*>(t);
-  float c = 0.f;
+  float c = 0.f, bad = 0.f;
   for (long base = threadIdx.x; base < NV; base += 8 * 1024) {
     T v[8];
 #pragma unroll
@@ -54,12 +52,23 @@ __global__ __launch_bounds__(1024) void count_valid_kernel(const int64_t* __rest
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (base + u * 1024 < NV) c += n_valid<T>(v[u], ignore);
+      if (base + u * 1024 < NV) {
+        if constexpr (PER == 2) {
+          tgt_count(v[u][0], ignore, V, c, bad);
+          tgt_count(v[u][1], ignore, V, c, bad);
+        } else {
+          tgt_count(v[u], ignore, V, c, bad);
+        }
+      }
   }
   if (threadIdx.x == 0)
-    for (long i = NV * PER; i < N; ++i) c += (t[i] != ignore) ? 1.f : 0.f;
+    for (long i = NV * PER; i < N; ++i) tgt_count(t[i], ignore, V, c, bad);
   c = block_sum<16>(c, red);
-  if (threadIdx.x == 0) inv_n[0] = 1.f / fmaxf(c, 1.f);
+  bad = block_sum<16>(bad, red);
+  if (threadIdx.x == 0) {
+    inv_n[0] = 1.f / fmaxf(c, 1.f);
+    if (bad > 0.f) err[0] = 1;
+  }
 }
 
 // Occupancy: the row lives in registers (CH x 4 VGPRs), so the VGPR budget decides how
@@ -102,7 +111,7 @@ __global__ __launch_bounds__(XT, (XT == 512 ? 4 : 2)) void xent_fwd_bwd_kernel(
   // output is bf16 anyway) so pass 3 does not recompute it; four sum chains
   const float m2 = m * L2E;
   const long tgt = targets[row];
-  const bool valid = tgt != ignore;
+  const bool valid = tgt != ignore && tgt >= 0 && tgt < V;  // see count_valid_kernel
   // the thread whose 16-byte chunks hold the target logit owns the loss (one scalar
   // re-read of that logit; a per-element compare against the target would cost a select
   // per logit)
@@ -166,12 +175,12 @@ using namespace orion;
 
 // logits (N, V) bf16 is overwritten with dlogits; scratch: losses[N] fp32, inv_n[1] fp32.
 int orion_xent_fwd_bwd(void* logits, const int64_t* targets, float* losses, float* inv_n,
-                       float* loss_out, long N, int V, long ignore, hipStream_t st) {
+                       float* loss_out, long N, int V, long ignore, int* err, hipStream_t st) {
   if (V % 8) return -1;
   if ((reinterpret_cast<uintptr_t>(targets) & 15) == 0)
-    count_valid_kernel<i64x2><<<1, 1024, 0, st>>>(targets, N, ignore, inv_n);
+    count_valid_kernel<i64x2><<<1, 1024, 0, st>>>(targets, N, ignore, V, inv_n, err);
   else
-    count_valid_kernel<int64_t><<<1, 1024, 0, st>>>(targets, N, ignore, inv_n);
+    count_valid_kernel<int64_t><<<1, 1024, 0, st>>>(targets, N, ignore, V, inv_n, err);
   auto L = (bf16_t*)logits;
   const int c512 = (V / 8 + 511) / 512, c1024 = (V / 8 + 1023) / 1024;
   if (c512 <= 13) {

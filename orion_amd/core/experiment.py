@@ -57,6 +57,40 @@ def utcnow():
     return n.replace(microsecond=n.microsecond // 1000 * 1000)
 
 
+def _proc_start_time(pid):
+    """Start time of ``pid`` in clock ticks since boot (``/proc/<pid>/stat`` field 22), or
+    None where /proc is unavailable."""
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as f:
+            stat = f.read().decode(errors="replace")
+        return int(stat[stat.rindex(")") + 2:].split()[19])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+_IDENTITY = {}
+
+
+def process_identity():
+    """Who owns a budget claim: host name, boot id, pid-namespace inode, pid and the pid's
+    start time.  Two processes are comparable by pid only when host, boot and pidns agree."""
+    pid = os.getpid()
+    if pid not in _IDENTITY:
+        try:
+            with open("/proc/sys/kernel/random/boot_id") as f:
+                boot = f.read().strip()
+        except OSError:
+            boot = None
+        try:
+            pidns = os.stat("/proc/self/ns/pid").st_ino
+        except OSError:
+            pidns = None
+        _IDENTITY.clear()
+        _IDENTITY[pid] = {"host": socket.gethostname(), "boot": boot, "pidns": pidns, "pid": pid,
+                          "start": _proc_start_time(pid)}
+    return dict(_IDENTITY[pid])
+
+
 class Experiment:
     __slots__ = ("name", "refers", "metadata", "pool_size", "max_trials", "status", "algorithms",
                  "_db", "_init_done", "_id", "_last_fetched", "_seen", "template", "_user")
@@ -170,6 +204,9 @@ class Experiment:
     # a claim whose owner cannot be probed (another host) is presumed dead after this long by
     # the writer's clock; owners on this host are probed by pid and recovered only when dead
     CLAIM_FOREIGN_GRACE_S = 3600.0
+    # an inserting claim (its producer passed confirm_claim) is left alone this long after the
+    # confirmation even when its owner looks dead: the insert of pool_size documents takes ms
+    CLAIM_INSERT_GRACE_S = 120.0
 
     def _budgeted(self):
         return self.max_trials not in (None, float("inf")) and self._id is not None
@@ -225,8 +262,7 @@ class Experiment:
                 return 0, None
             cid = uuid.uuid4().hex
             claims = dict(b.get("claims") or {})
-            claims[cid] = {"n": int(k), "host": socket.gethostname(), "pid": os.getpid(),
-                           "owner": owner, "t": utcnow(), "stage": "suggest"}
+            claims[cid] = dict(process_identity(), n=int(k), owner=owner, t=utcnow(), stage="suggest")
             if self._budget_cas(b, int(b["used"]) + k, claims):
                 return k, cid
         log.warning("trial budget: no token after %d attempts (heavy contention)", self.BUDGET_ATTEMPTS)
@@ -257,14 +293,27 @@ class Experiment:
         presumed dead), in which case the caller must not insert its trials."""
         if cid is None:
             return True
-        return self._update_claim(cid, lambda b, c: (int(b["used"]), dict(c, stage="insert")))
+        # ``t`` restarts here: an insert-stage claim is recovered only INSERT_GRACE_S after it
+        return self._update_claim(cid, lambda b, c: (int(b["used"]), dict(c, stage="insert", t=utcnow())))
 
-    def settle_budget(self, cid, inserted):
+    def _claim_trials_found(self, cid, n):
+        """How many of claim ``cid``'s ``n`` trials exist, in ANY status: a broken one already
+        gave its token back through :meth:`set_trial_status`, so it must not be returned twice."""
+        ids = [self.claim_trial_id(cid, i) for i in range(int(n))]
+        return self._db.count("trials", {"experiment": self._id, "_id": {"$in": ids}})
+
+    def settle_budget(self, cid, inserted=None):
         """Close claim ``cid`` after ``inserted`` of its trials were registered: the rest of its
-        tokens go back.  A no-op when the claim was already recovered."""
+        tokens go back.  ``inserted=None`` (the insert raised part-way) counts the claim's trials
+        in the store instead of trusting the caller.  A no-op when the claim was already
+        recovered."""
         if cid is None:
             return
-        self._update_claim(cid, lambda b, c: (max(0, int(b["used"]) - (int(c["n"]) - int(inserted))), None))
+
+        def fn(b, c):
+            got = self._claim_trials_found(cid, c["n"]) if inserted is None else int(inserted)
+            return max(0, int(b["used"]) - max(0, int(c["n"]) - got)), None
+        self._update_claim(cid, fn)
 
     def claim_budget(self, n):
         """Anonymous tokens (no claim record): up to ``n``; see :meth:`take_budget`."""
@@ -286,14 +335,28 @@ class Experiment:
 
     @classmethod
     def _claim_owner_dead(cls, c, now, grace_s):
-        if c.get("host") == socket.gethostname() and c.get("pid"):
+        """Whether claim ``c``'s producer is gone.  The owner is probed only when it provably
+        shares this process's pid space: same host name, boot id AND pid-namespace inode
+        (containers with host networking share a host name but not pids).  A live pid whose
+        start time differs from the recorded one is a reused pid, i.e. a dead owner.  Any
+        other owner is presumed dead ``grace_s`` after the claim's last stamp.  A claim already
+        inserting (stage ``insert``) is never recovered within :attr:`CLAIM_INSERT_GRACE_S` of
+        its confirmation, whatever the probe says."""
+        t = c.get("t")
+        age = None if t is None else (now - t).total_seconds()
+        if c.get("stage") == "insert" and (age is None or age <= cls.CLAIM_INSERT_GRACE_S):
+            return False
+        me = process_identity()
+        if (c.get("pid") and all(c.get(k) is not None and c.get(k) == me[k]
+                                 for k in ("host", "boot", "pidns"))):
+            pid = int(c["pid"])
             try:
-                os.kill(int(c["pid"]), 0)
+                os.kill(pid, 0)
             except OSError as e:
                 return e.errno == errno.ESRCH
-            return False
-        t = c.get("t")
-        return t is not None and now - t > datetime.timedelta(seconds=grace_s)
+            start = c.get("start")
+            return start is not None and _proc_start_time(pid) not in (None, start)
+        return age is not None and age > grace_s
 
     def reconcile_budget(self, grace_s=None):
         """Recover the tokens of claims whose producer died between taking them and settling:
@@ -311,10 +374,7 @@ class Experiment:
         got = 0
         for cid in dead:
             def fn(b, c, cid=cid):
-                ids = [self.claim_trial_id(cid, i) for i in range(int(c["n"]))]
-                found = self._db.count("trials", {"experiment": self._id, "_id": {"$in": ids},
-                                                  "status": {"$in": list(self.LIVE_STATI)}})
-                back = int(c["n"]) - found
+                back = max(0, int(c["n"]) - self._claim_trials_found(cid, c["n"]))
                 fn.back = back
                 return max(0, int(b["used"]) - back), None
             fn.back = 0

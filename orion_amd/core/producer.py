@@ -62,6 +62,7 @@ class Producer:
                 for i, t in enumerate(trials):
                     t._id = self.experiment.claim_trial_id(cid, i)
             log.debug("registering %d new trial(s)", len(trials))
+            inserted = None  # unknown until the insert returns: settle counts the store
             self.experiment.register_trials(trials)
             inserted = len(trials)
         finally:

@@ -43,8 +43,9 @@ def check_ids(idx, V):
 
 
 def id_error(device=None) -> bool:
-    """True if an embedding kernel saw an out-of-range token id since the last call on this
-    device (the flag is cleared; synchronises the current stream)."""
+    """True if an embedding kernel saw an out-of-range token id, or a cross-entropy kernel an
+    out-of-range target (not ignore_index; ``ops.xent.check_targets``), since the last call on
+    this device (the flag is cleared; synchronises the current stream)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     return bool(C().embed_id_error(dev.index if dev.index is not None else 0))
 

@@ -101,22 +101,49 @@ def _hip_eligible(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
 # reducer over more than one rank (ORION_GEMM_DDP_PERSISTENT=1 keeps the persistent walk);
 # the per-item walk costs 1-6 % on the isolated GPT-2 shapes
 # (profiles/ab/gemm16_persistent_stagger_peritem_r04.log, column cfgs_TFs).
-_PER_ITEM = False
+_PER_ITEM = False      # the explicit setting (set_per_item_walk)
+_PER_ITEM_REFS = 0     # live requests (request_per_item_walk): DDP trainers over > 1 rank
+
+
+def _apply_walk():
+    on = _PER_ITEM or _PER_ITEM_REFS > 0
+    cur = C().gemm_diag(-1)  # query
+    C().gemm_diag((cur | 64) if on else (cur & ~64))
 
 
 def set_per_item_walk(on: bool) -> bool:
-    """Select gemm16's one-workgroup-per-item walk (True) or the persistent walk (False).
-    Only the walk bit (64) of the diagnostic flags changes; returns the previous setting."""
+    """Select gemm16's one-workgroup-per-item walk (True) or the persistent walk (False) as the
+    explicit setting; live :func:`request_per_item_walk` requests keep the per-item walk on
+    regardless.  Only the walk bit (64) of the diagnostic flags changes; returns the previous
+    explicit setting."""
     global _PER_ITEM
     prev = _PER_ITEM
     _PER_ITEM = bool(on)
-    cur = C().gemm_diag(-1)  # query
-    C().gemm_diag((cur | 64) if _PER_ITEM else (cur & ~64))
+    _apply_walk()
     return prev
 
 
+def request_per_item_walk():
+    """Turn the per-item walk on for as long as the returned release callable has not run
+    (reference counted: overlapping requesters -- two DDP trainers, say -- keep it on until
+    the LAST one releases; then the explicit setting comes back).  The release is idempotent."""
+    global _PER_ITEM_REFS
+    _PER_ITEM_REFS += 1
+    _apply_walk()
+    done = []
+
+    def release():
+        global _PER_ITEM_REFS
+        if done:
+            return
+        done.append(1)
+        _PER_ITEM_REFS -= 1
+        _apply_walk()
+    return release
+
+
 def per_item_walk() -> bool:
-    return _PER_ITEM
+    return _PER_ITEM or _PER_ITEM_REFS > 0
 
 
 def _hip_wins(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:

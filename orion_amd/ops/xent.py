@@ -28,6 +28,7 @@ _LM_WGRAD_FIRST = os.environ.get("ORION_LMHEAD_WGRAD_FIRST", "1" if WGRAD_FIRST 
 class _LinearXent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, targets, ignore_index):
+        check_targets(targets, w.shape[0], int(ignore_index))
         logits = linear_fwd(x, w)
         loss = C().xent_fwd_bwd(logits, targets.contiguous(), int(ignore_index))
         ctx.save_for_backward(x, w, logits)   # logits now hold dlogits / n_valid
@@ -60,6 +61,26 @@ def linear_cross_entropy_hip(x, w, targets, ignore_index=-1):
     if lmhead_exp_eligible(x, w):
         return _LinearXentExp.apply(x, w, targets, ignore_index)
     return _LinearXent.apply(x, w, targets, ignore_index)
+
+
+_TGT_CHECK_ALWAYS = os.environ.get("ORION_CHECK_IDS") == "1"
+_tgt_checked: set = set()
+
+
+def check_targets(targets, V, ignore_index):
+    """Raise IndexError, as torch's cross_entropy does, when a target other than
+    ``ignore_index`` lies outside [0, V).  Host check (one sync) on the first call per device,
+    or on every call with ORION_CHECK_IDS=1; after that both kernels skip such a target (no
+    loss, no gradient, not counted in n_valid) and raise the device flag read by
+    ``ops.embedding.id_error``."""
+    key = targets.device
+    if key in _tgt_checked and not _TGT_CHECK_ALWAYS:
+        return
+    _tgt_checked.add(key)
+    bad = (targets != ignore_index) & ((targets < 0) | (targets >= V))
+    if bool(bad.any()):
+        t = targets[bad][0].item()
+        raise IndexError(f"Target {t} is out of bounds for {V} classes (ignore_index={ignore_index})")
 
 
 _LMHEAD = os.environ.get("ORION_LMHEAD", "exp")
@@ -104,6 +125,7 @@ class _LinearXentExp(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, targets, ignore_index):
         t = targets.contiguous()
+        check_targets(t, w.shape[0], int(ignore_index))
         loss, e, invz, inv_n = C().lmhead_fwd(x, w, t, int(ignore_index), _cref(x.device, w))
         ctx.save_for_backward(x, w, t, e, invz, inv_n)
         ctx.ignore = int(ignore_index)
@@ -136,6 +158,7 @@ class _LinearXentExp(torch.autograd.Function):
 class _Xent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, targets, ignore_index):
+        check_targets(targets, logits.shape[-1], int(ignore_index))
         buf = logits.detach().contiguous().clone()
         loss = C().xent_fwd_bwd(buf, targets.contiguous(), int(ignore_index))
         ctx.save_for_backward(buf)

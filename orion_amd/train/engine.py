@@ -133,9 +133,10 @@ class Trainer:
         if (self.reducer is not None and dev.type == "cuda" and dist.get_world_size() > 1
                 and os.environ.get("ORION_GEMM_DDP_PERSISTENT") != "1"):
             import weakref
-            from ..ops.gemm import set_per_item_walk
-            # scoped to this trainer: the previous walk comes back when it is collected
-            weakref.finalize(self, set_per_item_walk, set_per_item_walk(True))
+            from ..ops.gemm import request_per_item_walk
+            # scoped to this trainer (reference counted across trainers): the explicit walk
+            # comes back when the last requesting trainer is collected
+            weakref.finalize(self, request_per_item_walk())
         self.graph_enabled = bool(graph) and dev.type == "cuda" and self.reducer is None
         self._graph = None
         self._static = None

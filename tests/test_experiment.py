@@ -1,6 +1,7 @@
 """Experiment / producer / reservation protocol on local stores
 (reference: tests/unittests/core/test_experiment.py, test_producer.py)."""
 import datetime
+import os
 
 import pytest
 
@@ -320,3 +321,77 @@ def test_settle_after_recovery_is_a_noop(storage):
     exp.settle_budget(cid, 0)
     assert storage.read("experiments", {"_id": exp.id})[0]["budget"]["used"] == 0
     assert exp.take_budget(9)[0] == 4
+
+
+# ---------------------------------------------------------------- claim owners
+def _edit_claim(storage, exp, cid, **kw):
+    b = storage.read("experiments", {"_id": exp.id})[0]["budget"]
+    b["claims"][cid].update(kw)
+    storage.write("experiments", {"budget": b}, {"_id": exp.id})
+
+
+def test_claim_in_another_pid_namespace_is_not_probed(storage):
+    """Same host name, other pid namespace (host-networking containers): a pid that does not
+    exist HERE says nothing about the owner, so only the grace period recovers the claim."""
+    exp = _ready(storage, max_trials=4, pool_size=2)
+    k, cid = exp.take_budget(2, owner="ns")
+    _edit_claim(storage, exp, cid, pid=2 ** 22 + 12345, pidns=-1)
+    assert exp.reconcile_budget() == 0
+    _edit_claim(storage, exp, cid, t=utcnow() - datetime.timedelta(hours=2))
+    assert exp.reconcile_budget() == 2
+
+
+def test_reused_pid_counts_as_dead_owner(storage):
+    """The claim's pid is alive but started at another time: a reused pid, the owner is gone."""
+    exp = _ready(storage, max_trials=4, pool_size=2)
+    k, cid = exp.take_budget(2, owner="reused")
+    me = storage.read("experiments", {"_id": exp.id})[0]["budget"]["claims"][cid]
+    assert me["pid"] == os.getpid() and me["start"] is not None
+    assert exp.reconcile_budget() == 0  # alive, same start time
+    _edit_claim(storage, exp, cid, start=me["start"] - 1)
+    assert exp.reconcile_budget() == 2
+
+
+def test_inserting_claim_waits_for_its_grace(storage):
+    """A confirmed (insert-stage) claim is never recovered within CLAIM_INSERT_GRACE_S of the
+    confirmation, even when its owner probes dead; a broken trial of the claim counts as
+    accounted for (it already returned its token)."""
+    import subprocess
+    import sys
+    exp = _ready(storage, max_trials=4, pool_size=4)
+    k, cid = exp.take_budget(3, owner="ins")
+    assert exp.confirm_claim(cid)
+    p = subprocess.Popen([sys.executable, "-c", "pass"])
+    p.wait()
+    _edit_claim(storage, exp, cid, pid=p.pid)
+    ts = []
+    for i in range(2):
+        t = Trial(params=[dict(name="/x", type="real", value=float(i))])
+        t._id = exp.claim_trial_id(cid, i)
+        ts.append(t)
+    exp.register_trials(ts)
+    assert exp.set_trial_status(ts[1], "broken")  # gives its token back: used 3 -> 2
+    assert exp.reconcile_budget() == 0
+    old = utcnow() - datetime.timedelta(seconds=exp.CLAIM_INSERT_GRACE_S + 5)
+    _edit_claim(storage, exp, cid, t=old)
+    assert exp.reconcile_budget() == 1  # only the never-inserted third trial
+    b = storage.read("experiments", {"_id": exp.id})[0]["budget"]
+    assert b["used"] == 1 and b["claims"] == {}
+
+
+def test_settle_counts_the_store_when_insert_failed(storage, monkeypatch):
+    """An insert that raised part-way: settle counts the claim's trials instead of trusting
+    the producer's local count (0), so the written trials keep their tokens."""
+    exp = _ready(storage, max_trials=4, pool_size=3)
+    prod = Producer(exp)
+    real = Experiment.register_trials
+
+    def partial(self, trials):
+        real(self, trials[:2])
+        raise RuntimeError("connection lost")
+    monkeypatch.setattr(Experiment, "register_trials", partial)
+    with pytest.raises(RuntimeError):
+        prod.produce()
+    b = storage.read("experiments", {"_id": exp.id})[0]["budget"]
+    assert b["used"] == 2 and b["claims"] == {}
+    assert exp.count_trials("new") == 2

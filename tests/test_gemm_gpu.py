@@ -337,3 +337,23 @@ def test_per_item_walk_is_bitwise_identical():
             G.set_per_item_walk(False)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_per_item_walk_requests_are_reference_counted():
+    """overlapping DDP trainers each request the per-item walk; releasing the older
+    one must not switch the walk back while the newer one is alive."""
+    from orion_amd.ops import gemm as G
+    G.set_per_item_walk(False)
+    r1 = G.request_per_item_walk()
+    r2 = G.request_per_item_walk()
+    try:
+        assert G.per_item_walk() and (_C().gemm_diag(-1) & 64)
+        r1()
+        r1()  # idempotent
+        assert G.per_item_walk() and (_C().gemm_diag(-1) & 64)
+        r2()
+        assert not G.per_item_walk() and not (_C().gemm_diag(-1) & 64)
+    finally:
+        r1()
+        r2()
+        G.set_per_item_walk(False)

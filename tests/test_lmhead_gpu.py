@@ -158,3 +158,31 @@ def test_lmhead_exp_llama_vocab_bwd_order():
                       (want[0].reshape(1), want[1], want[2]), ((lb / 2.0).detach().reshape(1), *gb))
     finally:
         X._LM_WGRAD_FIRST = old
+
+
+@pytest.mark.parametrize("path", ["exp", "rowpass"])
+def test_out_of_range_target_raises_and_is_skipped(path, monkeypatch):
+    """a target outside [0, V) that is not ignore_index raises IndexError on the
+    host check (as torch's cross_entropy does); past the check, both kernels use ONE validity
+    rule -- the row is skipped, not counted in n_valid -- and raise the device flag."""
+    from orion_amd.ops import embedding as emb
+    monkeypatch.setattr(X, "_LMHEAD", path)
+    V, C = 1152, 256
+    x, w, t = _case(256, V, C, False, seed=3)
+    t[10] = V + 5
+    t[20] = -100   # ignore_index is -1 here, so -100 is out of range, not ignored
+    X._tgt_checked.discard(t.device)
+    with pytest.raises(IndexError):
+        ops.linear_cross_entropy(x, w, t, ignore_index=-1)
+    assert not emb.id_error(DEV)
+    x.grad = w.grad = None
+    loss = ops.linear_cross_entropy(x, w, t, ignore_index=-1)  # checked once per device
+    loss.backward()
+    torch.cuda.synchronize()
+    assert emb.id_error(DEV)
+    keep = t.clone()
+    keep[10] = keep[20] = -1
+    want = _ref(x, w, keep, 1.0)
+    assert rel_err(loss.float(), want[0]) < 2e-2
+    assert rel_err(x.grad.float(), want[1]) < 5e-2
+    assert float(x.grad[10].float().abs().max()) == 0.0 and float(x.grad[20].float().abs().max()) == 0.0
