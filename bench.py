@@ -77,6 +77,9 @@ def parse():
                          "next forward).  auto (default): on for models of >= 1B parameters at "
                          "N > 1 GPUs; a bare --zero1 = on (with one GPU: a world-1 rehearsal of "
                          "the sharded path)")
+    ap.add_argument("--tied-bf16", action="store_true",
+                    help="N > 1: reduce GPT-2's tied wte bucket split -- the LM head's part in fp32 under "
+                         "the backward, the embedding's part in bf16 after it (parallel/ddp.py)")
     ap.add_argument("--per-item-walk", action="store_true",
                     help="force gemm16's one-workgroup-per-item walk (what multi-rank training selects "
                          "so RCCL kernels get CUs) also at N = 1: separates that walk's cost from the "
@@ -175,7 +178,8 @@ def main():
     if args.impl == "native":
         trainer = Trainer(model, ocfg, bucket_mb=args.bucket_mb, graph=args.hip_graph and world == 1,
                           grad_dtype=torch.float32 if args.grad_dtype == "fp32" else torch.bfloat16,
-                          ddp_timing=world > 1, zero1={"auto": None, "on": True, "off": False}[args.zero1])
+                          ddp_timing=False, zero1={"auto": None, "on": True, "off": False}[args.zero1],
+                          tied_bf16=args.tied_bf16)
         step_fn = lambda i: trainer.step([pool[(i * A + j) % 4] for j in range(A)])
         if args.per_item_walk and dev.type == "cuda":
             from orion_amd.ops.gemm import set_per_item_walk
@@ -235,6 +239,12 @@ def main():
         elapsed = float(t)
     final_loss = float(loss)
     busbw = ddp = rccl = replicas = None
+    if world > 1 and args.impl == "native" and trainer.reducer is not None:
+        # the bucket timeline comes from ONE extra step after the timed region: the timed steps
+        # run without the per-bucket events and the side-stream waits they need
+        trainer.reducer.timing = True
+        step_fn(args.warmup + args.steps)
+        sync()
     if args.check_replicas and args.impl == "native":
         mine = _replica_checksums(trainer, dev)
         if world > 1:
@@ -245,7 +255,7 @@ def main():
         replicas = {"identical": all(torch.equal(c, allc[0]) for c in allc),
                     "checksums": [round(float(x), 6) for x in allc[0].tolist()]}
     if world > 1 and args.impl == "native":
-        # bucket timeline of the last timed step: launch -> complete per bucket, exposed tail
+        # bucket timeline of the extra step: launch -> complete per bucket, exposed tail
         ddp = trainer.reducer.timing_report()
         if ddp is not None:
             t = torch.tensor([ddp["exposed_tail_ms"], ddp["comm_ms"]], device=dev, dtype=torch.float64)
@@ -296,6 +306,8 @@ def main():
             "dist_backend": args.dist_backend if world > 1 or args.zero1 == "on" else None,
             "zero1": bool(args.impl == "native" and trainer.zero1),
             "zero1_mode": args.zero1,
+            "tied_bf16": bool(args.tied_bf16 and args.impl == "native" and world > 1
+                              and trainer.reducer is not None and bool(trainer.reducer.tails)),
             "gemm16_walk": ("per_item" if args.impl == "native" and dev.type == "cuda" and _per_item_walk()
                             else "persistent"),
             "optimizer_state_gb_per_rank": (round(3 * 4 * trainer.opt.master.numel() / 2**30, 2)

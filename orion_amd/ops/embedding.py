@@ -102,17 +102,18 @@ class _EmbedLayerNorm(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             st = sink_of(wte)
             if st is not None and st.view.dtype == torch.float32 and not deterministic():
-                acc = st.take()
+                view, acc = st.last_use_target()
                 if not acc:  # first producer of the step: the slice is not pre-zeroed
-                    st.view.zero_()
-                C().embed_scatter_add_(dx2, idx, st.view.view(-1, Cc))
+                    view.zero_()
+                C().embed_scatter_add_(dx2, idx, view.view(-1, Cc))
                 st.notify(last=True)
             elif st is not None:
                 g = _dense_table_grad(dx2, idx, wte.shape[0])
-                if st.take():
-                    st.view.view(-1, Cc).add_(g)
+                view, acc = st.last_use_target()
+                if acc:
+                    view.view(-1, Cc).add_(g)
                 else:
-                    st.view.view(-1, Cc).copy_(g)
+                    view.view(-1, Cc).copy_(g)
                 st.notify(last=True)
             else:
                 dwte = _dense_table_grad(dx2, idx, wte.shape[0]).to(wte.dtype)
@@ -151,18 +152,19 @@ class _Embedding(torch.autograd.Function):
             dy2 = dy2.to(torch.bfloat16)
         st = sink_of(wte)
         if st is not None and st.view.dtype == torch.float32 and not deterministic():
-            acc = st.take()
+            view, acc = st.last_use_target()
             if not acc:  # first producer of the step: the slice is not pre-zeroed
-                st.view.zero_()
-            C().embed_scatter_add_(dy2, idx, st.view.view(-1, Cc))
+                view.zero_()
+            C().embed_scatter_add_(dy2, idx, view.view(-1, Cc))
             st.notify(last=True)
             return None, None
         if st is not None:
             g = _dense_table_grad(dy2, idx, wte.shape[0])
-            if st.take():
-                st.view.view(-1, Cc).add_(g)
+            view, acc = st.last_use_target()
+            if acc:
+                view.view(-1, Cc).add_(g)
             else:
-                st.view.view(-1, Cc).copy_(g)
+                view.view(-1, Cc).copy_(g)
             st.notify(last=True)
             return None, None
         return None, _dense_table_grad(dy2, idx, wte.shape[0]).to(wte.dtype)

@@ -41,7 +41,7 @@ ENABLED = os.environ.get("ORION_DIRECT_GRADS", "1") != "0"
 
 class GradSink:
     __slots__ = ("view", "fresh", "expect", "notes", "_micro", "_param", "_listeners",
-                 "__weakref__")
+                 "tail", "tail_cb", "__weakref__")
 
     def __init__(self, param: torch.Tensor, view: torch.Tensor, listeners: list, expect: int = 1):
         self.view = view            # the parameter's slice of the gradient arena, param-shaped
@@ -51,6 +51,13 @@ class GradSink:
         self._micro = 0             # notify() calls since the last use's notify(last=True)
         self._param = weakref.ref(param)
         self._listeners = listeners  # shared with the owning arena
+        # split tied gradient (parallel/ddp.py, tied_bf16): while set by the data-parallel
+        # reducer, the LAST use writes its contribution here (param-shaped fp32, overwritten)
+        # instead of accumulating into ``view``, the earlier uses' notify() reports the
+        # parameter at once (its arena bucket can be reduced under the rest of the backward)
+        # and the last use's notify(last=True) calls ``tail_cb(param)``
+        self.tail = None
+        self.tail_cb = None
 
     def reset(self):
         """Start of an optimizer step (the arena's zero_grad)."""
@@ -64,11 +71,30 @@ class GradSink:
         self.fresh = False
         return acc
 
+    def last_use_target(self):
+        """(tensor, accumulate) for the parameter's LAST use (the embedding of a tied table):
+        the split tail when the reducer set one (overwrite), else the arena slice
+        (``take()``)."""
+        if self.tail is not None:
+            return self.tail, False
+        return self.view, self.take()
+
     def notify(self, last: bool = False):
         """One producer wrote its gradient through the sink.  ``last``: the producer is the
         parameter's last use in the backward (only meaningful for tied parameters)."""
         self.notes += 1
         self._micro += 1
+        if self.expect > 1 and self.tail is not None:
+            p = self._param()
+            if p is None:
+                return
+            if last:
+                self._micro = 0
+                self.tail_cb(p)
+            else:
+                for cb in self._listeners:
+                    cb(p)
+            return
         if self.expect > 1:
             if not last:
                 return

@@ -23,6 +23,11 @@ Design (MI355X-first, not a translation of any NCCL call pattern):
 * a tied parameter (GPT-2's ``wte`` = LM head) starts a bucket of its own: its
   gradient is complete only after the embedding backward, the last kernel of the
   pass, and would otherwise hold back every layer sharing its bucket;
+* split tied gradient (``tied_bf16``, opt-in): the tied bucket is reduced as soon as the
+  LM head has written its part (under the whole backward), and only the embedding's part --
+  written by the last kernel into a separate fp32 tail -- is reduced after the backward, in
+  bf16 on the wire: the exposed bytes of GPT-2-124M's 154.5 MB tied bucket halve, and the
+  LM head's (larger, denser) contribution keeps fp32 precision;
 * gradient accumulation: reduction is only armed on the last micro-step
   (``set_sync``), the same contract as DDP's ``no_sync``;
 * observability (``timing=True``): per bucket, the moment its gradients were ready on the
@@ -122,9 +127,27 @@ class _Watchdog(threading.Thread):
                 os._exit(124)
 
 
+class _TiedTail:
+    """The split last-use contribution of one tied parameter (``tied_bf16``): ``buf`` spans the
+    parameter's whole bucket (fp32, zero outside the parameter, so a ZeRO-1 reduce-scatter of
+    it shards like the bucket), ``view`` is the parameter-shaped slice the embedding backward
+    writes, ``wire`` the bf16 copy that is reduced."""
+
+    def __init__(self, bucket, b0, b1, slot, sink, device):
+        self.bucket, self.b0, self.b1, self.slot, self.sink = bucket, b0, b1, slot, sink
+        self.buf = torch.zeros(b1 - b0, dtype=torch.float32, device=device)
+        self.view = self.buf[slot.offset - b0: slot.offset - b0 + slot.numel].view_as(slot.param)
+        self.wire = torch.zeros(b1 - b0, dtype=torch.bfloat16, device=device)
+        self.out = None          # ZeRO-1: this rank's reduced piece
+        self.ready = False
+        self.handle = None
+        self.t_ready = self.t_done = None
+
+
 class GradBucketReducer:
     def __init__(self, arena: FlatArena, bucket_mb: float | None = None, group=None,
-                 average: bool = True, timing: bool = False, watchdog_s: float | None = None):
+                 average: bool = True, timing: bool = False, watchdog_s: float | None = None,
+                 tied_bf16: bool = False):
         if bucket_mb is None or bucket_mb <= 0:
             bucket_mb = default_bucket_mb(arena.numel)
         self.arena = arena
@@ -151,7 +174,7 @@ class GradBucketReducer:
         self._arrived = [set() for _ in self.buckets]
         self._handles = [None] * len(self.buckets)
         self._ready = [False] * len(self.buckets)
-        self._cursor = 0                 # next bucket index allowed to launch
+        self._cursor = 0                 # position in self._order of the next bucket to launch
         self.launch_log: list[int] | None = None  # tests: bucket indices in launch order
         self._sync = True
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._on_grad)
@@ -175,6 +198,23 @@ class GradBucketReducer:
         if watchdog_s > 0 and self.world > 1:
             self._watchdog = _Watchdog(watchdog_s, dist.get_rank(group))
             self._watchdog.start()
+        # split tied gradients (module docstring): one tail per tied parameter whose gradient
+        # goes through an fp32 arena sink (the GPU path; see ops/grad_sink.py)
+        self.tails: list[_TiedTail] = []
+        if tied_bf16:
+            for bi, (b0, b1, slots) in enumerate(self.buckets):
+                for sl in slots:
+                    sk = getattr(sl.param, "_orion_sink", None)
+                    if (id(sl.param) in getattr(arena, "shared", set()) and sk is not None
+                            and sk.view.dtype == torch.float32 and sk.expect > 1):
+                        self.tails.append(_TiedTail(bi, b0, b1, sl, sk, arena.grads.device))
+        self._tail_cursor = 0
+        # launch order: bucket index order, except that a split tied bucket goes FIRST -- the
+        # LM head, which completes it, is the first kernel of the backward, while its arena
+        # position (the table is the model's first module) is last.  Any fixed permutation
+        # keeps every rank's collective sequence identical.
+        tied = [t.bucket for t in self.tails]
+        self._order = tied + [bi for bi in range(len(self.buckets)) if bi not in tied]
 
     # ------------------------------------------------------------------ timing
     def _mark(self):
@@ -202,16 +242,32 @@ class GradBucketReducer:
         for bi, (b0, b1, _) in enumerate(self.buckets):
             rows.append((bi, round((b1 - b0) * esize / 2**20, 2), round(rel(self._t_ready[bi]), 3),
                          round(rel(self._t_done[bi]), 3)))
+        tails = [(t.bucket, round(t.wire.numel() * t.wire.element_size() / 2**20, 2),
+                  round(rel(t.t_ready), 3), round(rel(t.t_done), 3))
+                 for t in self.tails if t.t_ready is not None and t.t_done is not None]
         bwd = rel(self._bwd_end)
-        last = max(r[3] for r in rows)
-        return {"buckets": rows, "bwd_end_ms": round(bwd, 3),
+        last = max(r[3] for r in rows + tails)
+        return {"buckets": rows, "tied_tails": tails, "bwd_end_ms": round(bwd, 3),
                 "exposed_tail_ms": round(max(0.0, last - bwd), 3),
-                "comm_ms": round(sum(r[3] - r[2] for r in rows), 3)}
+                "comm_ms": round(sum(r[3] - r[2] for r in rows + tails), 3)}
 
     # ------------------------------------------------------------------ control
     def set_sync(self, flag: bool):
-        """Arm (True) or disarm (False) reduction for the coming backward."""
+        """Arm (True) or disarm (False) reduction for the coming backward.  Armed, a tied
+        parameter's last use writes into its split tail (``tied_bf16``)."""
         self._sync = flag
+        for t in self.tails:
+            t.sink.tail = t.view if flag else None
+            t.sink.tail_cb = self._on_tail if flag else None
+
+    def _on_tail(self, p):
+        """The last use of tied parameter ``p`` wrote its tail (on the compute stream): make
+        the bf16 wire copy and launch it once every bucket has launched."""
+        for t in self.tails:
+            if t.slot.param is p:
+                t.wire.copy_(t.buf)
+                t.ready = True
+        self._flush()
 
     def broadcast_params(self, src=0):
         """R1: make every rank start from rank ``src``'s weights."""
@@ -235,10 +291,55 @@ class GradBucketReducer:
             self._flush()
 
     def _flush(self):
-        """Launch every ready bucket at the cursor, in index order."""
-        while self._cursor < len(self.buckets) and self._ready[self._cursor]:
-            self._launch(self._cursor)
+        """Launch every ready bucket at the cursor, in launch order (``_order``); the tied tails
+        go last, so every rank issues the same sequence of collectives."""
+        while self._cursor < len(self.buckets) and self._ready[self._order[self._cursor]]:
+            self._launch(self._order[self._cursor])
             self._cursor += 1
+        if self._cursor == len(self.buckets):
+            while self._tail_cursor < len(self.tails) and self.tails[self._tail_cursor].ready:
+                self._launch_tail(self.tails[self._tail_cursor])
+                self._tail_cursor += 1
+
+    def _tail_collective(self, t, op):
+        return dist.all_reduce(t.wire, op=op, group=self.group, async_op=True)
+
+    def _launch_tail(self, t):
+        if self.launch_log is not None:
+            self.launch_log.append(("tail", t.bucket))
+        op = dist.ReduceOp.AVG if self._use_avg_op else dist.ReduceOp.SUM
+        if self.timing:
+            t.t_ready = self._mark()
+        t.handle = self._tail_collective(t, op)
+        if self.timing and self._cuda:
+            if self._tstream is None:
+                self._tstream = torch.cuda.Stream()
+            with torch.cuda.stream(self._tstream):
+                t.handle.wait()
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(self._tstream)
+            t.t_done = ev
+        if self._watchdog is not None:
+            self._watchdog.add(self.step, f"tied tail of bucket {t.bucket}", t.handle, t.wire.numel())
+
+    def _finish_tails(self, add_into):
+        """Wait for the tails and add each (averaged) into ``add_into(t)`` (the fp32 gradient
+        the tail belongs to); a tied parameter whose last use wrote around its sink while the
+        split was armed is an error (its bucket was being reduced while it was written)."""
+        for t in self.tails:
+            if not t.ready:
+                if t.sink.notes:
+                    raise RuntimeError(
+                        f"tied_bf16: {t.slot.name}'s last use did not write through its gradient "
+                        "sink (an AccumulateGrad path?) -- run without ORION_DDP_TIED_BF16")
+                continue
+            t.handle.wait()
+            if self.timing and not self._cuda:
+                t.t_done = time.perf_counter()
+            src = t.out if t.out is not None else t.wire
+            add_into(t).add_(src, alpha=1.0 if self._use_avg_op else 1.0 / self.world)
+            t.ready, t.handle = False, None
+        self._tail_cursor = 0
 
     def _launch(self, bi):
         if self._handles[bi] is not None:
@@ -279,6 +380,7 @@ class GradBucketReducer:
             if self.average and not self._use_avg_op:
                 b0, b1, _ = self.buckets[bi]
                 self.arena.grads[b0:b1].div_(self.world)
+        self._finish_tails(lambda t: self.arena.grads[t.b0:t.b1])
         self._handles = [None] * len(self.buckets)
         self._arrived = [set() for _ in self.buckets]
         self._ready = [False] * len(self.buckets)
@@ -286,6 +388,8 @@ class GradBucketReducer:
         self.step += 1
 
     def remove(self):
+        for t in self.tails:
+            t.sink.tail = t.sink.tail_cb = None
         if self._watchdog is not None:
             self._watchdog.stop.set()
             self._watchdog = None
@@ -312,9 +416,9 @@ class ShardedGradReducer(GradBucketReducer):
     flat buffer and the fused AdamW kernel runs over them unchanged."""
 
     def __init__(self, arena: FlatArena, bucket_mb: float | None = None, group=None,
-                 timing: bool = False, watchdog_s: float | None = None):
+                 timing: bool = False, watchdog_s: float | None = None, tied_bf16: bool = False):
         super().__init__(arena, bucket_mb=bucket_mb, group=group, average=True, timing=timing,
-                         watchdog_s=watchdog_s)
+                         watchdog_s=watchdog_s, tied_bf16=tied_bf16)
         from ..train.flat import ALIGN
         self.rank = dist.get_rank(group)
         n = self.world
@@ -329,6 +433,8 @@ class ShardedGradReducer(GradBucketReducer):
             self.shard_ranges.append((bi, b0 + self.rank * piece, off, piece))
             off += piece
         self.shard_numel = off
+        for t in self.tails:
+            t.out = torch.zeros((t.b1 - t.b0) // n, dtype=torch.bfloat16, device=arena.grads.device)
         dev = arena.grads.device
         self.grad_shard = torch.zeros(off, dtype=arena.grads.dtype, device=dev)
         self.param_shard = torch.zeros(off, dtype=arena.params.dtype, device=dev)
@@ -395,6 +501,9 @@ class ShardedGradReducer(GradBucketReducer):
                 full[b0:b1].copy_(tmp[:b1 - b0])
         return full
 
+    def _tail_collective(self, t, op):
+        return dist.reduce_scatter_tensor(t.out, t.wire, op=op, group=self.group, async_op=True)
+
     def _on_grad(self, p):
         if self.check_gathers and self._sync and not any(self._arrived):
             pend = [bi for bi, h in enumerate(self._pgather) if h is not None]
@@ -444,6 +553,8 @@ class ShardedGradReducer(GradBucketReducer):
                 self._t_done[bi] = time.perf_counter()
         if not self._use_avg_op:
             self.grad_shard.div_(self.world)
+        so_of = {bi: (so, ln) for bi, _, so, ln in self.shard_ranges}
+        self._finish_tails(lambda t: self.grad_shard[so_of[t.bucket][0]:so_of[t.bucket][0] + so_of[t.bucket][1]])
         self._handles = [None] * len(self.buckets)
         self._arrived = [set() for _ in self.buckets]
         self._ready = [False] * len(self.buckets)

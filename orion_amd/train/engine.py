@@ -74,7 +74,7 @@ class Trainer:
     def __init__(self, model: torch.nn.Module, optim: OptimConfig | None = None,
                  ddp: bool | None = None, bucket_mb: float | None = None, arena_dtype=None,
                  graph: bool = False, grad_dtype=None, ddp_timing: bool = False,
-                 zero1: bool | None = None):
+                 zero1: bool | None = None, tied_bf16: bool | None = None):
         self.model = model
         self.cfg = optim or OptimConfig()
         dev = next(model.parameters()).device
@@ -93,6 +93,10 @@ class Trainer:
         # zero1=None (auto): sharded from ZERO1_AUTO_PARAMS parameters up when there is more
         # than one rank -- a 7B model's replicated fp32 master + Adam state is 81 GB per GPU and
         # its all-reduce moves 2 (N-1)/N x 27 GB of fp32 gradients per step
+        # split tied gradient with a bf16 tail on the wire (parallel/ddp.py; opt-in,
+        # ORION_DDP_TIED_BF16=1): halves the exposed bytes of GPT-2's tied wte bucket
+        if tied_bf16 is None:
+            tied_bf16 = os.environ.get("ORION_DDP_TIED_BF16") == "1"
         dist_on = dist.is_available() and dist.is_initialized()
         if zero1 is None:
             zero1 = (dist_on and dist.get_world_size() > 1
@@ -108,7 +112,8 @@ class Trainer:
             dist.broadcast(self.arena.init_fp32, 0)
             with torch.no_grad():
                 self.arena.params.copy_(self.arena.init_fp32)
-            self.reducer = ShardedGradReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing)
+            self.reducer = ShardedGradReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing,
+                                              tied_bf16=tied_bf16)
             self.reducer.install_gather_hooks(model)
             self.reducer.init_fp32 = self.reducer.shard_of(self.arena.init_fp32)
             self.arena.init_fp32 = None
@@ -123,7 +128,8 @@ class Trainer:
                                  weight_decay=self.cfg.weight_decay, grad_clip=self.cfg.grad_clip)
             if ddp:
                 from ..parallel.ddp import GradBucketReducer
-                self.reducer = GradBucketReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing)
+                self.reducer = GradBucketReducer(self.arena, bucket_mb=bucket_mb, timing=ddp_timing,
+                                                 tied_bf16=tied_bf16)
                 # R1: every rank starts from rank 0's exact fp32 weights
                 dist.broadcast(self.opt.master, 0)
                 with torch.no_grad():

@@ -277,3 +277,112 @@ def test_divergent_arrival_orders_and_unused_params_four_ranks():
         assert logs == [list(range(nb))] * 2, (rank, logs)
         assert timed
         assert torch.allclose(torch.from_numpy(grads), torch.full_like(torch.from_numpy(grads), 2.5))
+
+
+# ------------------------------------------------------------- split tied bucket (VERDICT r5 #5a)
+def _tied_worker(rank, world, port, zero1, out):
+    """One rank: GPT-2-tiny's arena (fp32 gradients) with a CPU-constructed sink on the tied
+    wte (the GPU path's sinks are CUDA-only), gradients written the way the GPU backward
+    writes them -- LM-head part through the sink first, every other parameter, then the
+    embedding's part as the tied parameter's last use -- reduced fp32-joint and split."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from orion_amd.ops.grad_sink import GradSink
+    from orion_amd.parallel.ddp import GradBucketReducer, ShardedGradReducer, zero1_pad_names
+    from orion_amd.train.flat import FlatArena
+    torch.manual_seed(0)
+    model = build_gpt2("gpt2-tiny", block_size=32)
+    res = {}
+    for split in (False, True):
+        kw = {}
+        if zero1:
+            names, pad_to = zero1_pad_names(model, 0.05, torch.float32, world)
+            kw = dict(pad_after=names, pad_to=pad_to)
+        arena = FlatArena(model, dtype=torch.float32, grad_dtype=torch.float32, **kw)
+        wte = model.transformer.wte.weight
+        slot = next(s_ for s_ in arena.slots if s_.param is wte)
+        sink = GradSink(wte, arena.grad_view(slot).view_as(wte), arena.grad_listeners, expect=2)
+        wte._orion_sink = sink
+        cls = ShardedGradReducer if zero1 else GradBucketReducer
+        red = cls(arena, bucket_mb=0.05, timing=True, watchdog_s=60.0, tied_bf16=split)
+        assert len(red.tails) == (1 if split else 0)
+        red.launch_log = []
+        g = torch.Generator().manual_seed(1000 + rank)
+        lm = torch.randn(wte.shape, generator=g)
+        emb = torch.zeros(wte.shape)
+        rows = torch.randint(0, wte.shape[0], (64,), generator=g)
+        emb.index_add_(0, rows, torch.randn(64, wte.shape[1], generator=g))
+        others = {s_.name: torch.randn(s_.numel, generator=g) for s_ in arena.slots if s_.param is not wte}
+        arena.zero_grad()
+        red.set_sync(True)
+        assert sink.take() is False
+        sink.view.copy_(lm)
+        sink.notify()                     # the LM head, first kernel of the backward
+        for s_ in arena.slots:
+            if s_.param is not wte:
+                arena.grad_view(s_).copy_(others[s_.name])
+                red._on_grad(s_.param)
+                time.sleep(0.002)         # a backward's worth of spacing for the timeline
+        view, acc = sink.last_use_target()
+        assert acc is (not split) and (view is not sink.view) is split
+        if acc:
+            view.add_(emb)
+        else:
+            view.copy_(emb)
+        sink.notify(last=True)            # the embedding, last kernel of the backward
+        red.finish()
+        rep = red.timing_report()
+        if zero1:
+            full = red.gather_full(red.grad_shard)
+        else:
+            full = arena.grads.clone()
+        res[split] = (full[slot.offset:slot.offset + slot.numel].numpy().copy(),
+                      full.numpy().copy(), rep, list(red.launch_log), slot.offset, slot.numel)
+        red.remove()
+        del wte._orion_sink
+    out.put((rank, res))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("zero1", [False, True])
+def test_tied_bucket_split_bf16_tail_eight_ranks(zero1):
+    """8 gloo ranks: with ``tied_bf16`` the tied bucket launches right after the LM head's
+    write (first, under the rest of the 'backward'), the embedding's part follows as a bf16
+    tail after every bucket, and the result equals the fp32 joint reduction within the bf16
+    budget of the tail alone (the other parameters bit-identical); the tail's wire bytes
+    are half the tied bucket's fp32 bytes."""
+    world = 8
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tied_worker, args=(r, world, port, zero1, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    joint_w, joint_all, rep0, log0, off, n = got[0][False]
+    split_w, split_all, rep1, log1, _, _ = got[0][True]
+    joint_w, joint_all, split_w, split_all = map(torch.from_numpy, (joint_w, joint_all, split_w, split_all))
+    for r in range(world):  # replicas agree
+        assert torch.equal(torch.from_numpy(got[r][True][1]), split_all)
+    # untouched parameters: identical; the tied one within bf16 rounding of the embedding part
+    mask = torch.ones_like(joint_all, dtype=torch.bool)
+    mask[off:off + n] = False
+    assert torch.equal(joint_all[mask], split_all[mask])
+    err = (split_w - joint_w).abs().max().item()
+    assert 0 < err <= 2e-2 * joint_w.abs().max().item(), err
+    # launch order: joint -- bucket index order, the tied bucket (the table's arena position
+    # is last) held until the embedding; split -- the tied bucket FIRST (right after the LM
+    # head's write), the others in index order, the bf16 tail after everything
+    tied_b = rep1["tied_tails"][0][0]
+    assert log0 == list(range(len(log0))) and log0[-1] == tied_b
+    assert log1 == [tied_b] + log0[:-1] + [("tail", tied_b)], log1
+    fp32_mb = rep0["buckets"][tied_b][1]
+    assert abs(rep1["tied_tails"][0][1] - fp32_mb / 2) < 0.02, (rep1["tied_tails"], fp32_mb)
+    # the timeline: split -- the tied bucket was ready before every other bucket; joint -- after
+    others = [r[2] for r in rep1["buckets"] if r[0] != tied_b]
+    assert rep1["buckets"][tied_b][2] <= min(others)
+    assert rep0["buckets"][tied_b][2] >= max(r[2] for r in rep0["buckets"] if r[0] != tied_b)

@@ -226,3 +226,74 @@ def test_zero1_overlapped_gather_on_rccl_matches_serial():
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "ZERO1 RCCL overlap ok" in r.stdout
+
+
+_TIED_BF16_RCCL = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ORION_REPO"])
+from orion_amd import ops
+from orion_amd.models import build_model
+from orion_amd.parallel.launch import init_process_group
+from orion_amd.train.engine import OptimConfig, Trainer
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+init_process_group("nccl", dev)
+ops.load_ext(required=True)
+cfg = OptimConfig(learning_rate=1e-3, warmup_iters=0, decay_lr=False, grad_clip=0.0)
+g = torch.Generator(device=dev).manual_seed(3)
+xb = [(torch.randint(0, 50257, (2, 64), device=dev, generator=g),
+       torch.randint(0, 50257, (2, 64), device=dev, generator=g)) for _ in range(2)]
+for zero1 in (False, True):
+    torch.manual_seed(0)
+    model = build_model("gpt2-tiny").to(dev)
+    tr = Trainer(model, cfg, ddp=True, bucket_mb=0.25, ddp_timing=True, tied_bf16=True, zero1=zero1)
+    assert len(tr.reducer.tails) == 1
+    tb = tr.reducer.tails[0].bucket
+    tr.reducer.launch_log = []
+    torch.manual_seed(0)
+    ref_model = build_model("gpt2-tiny").to(dev)
+    ref = Trainer(ref_model, cfg, ddp=False)
+    rslot = {s.name: s for s in ref.arena.slots}
+    for s in tr.arena.slots:   # same weights (ZeRO-1 pads its arena: copy slot by slot)
+        r = rslot[s.name]
+        ref.arena.params[r.offset:r.offset + r.numel].copy_(tr.arena.params[s.offset:s.offset + s.numel])
+    tr.step(xb)
+    ref.step(xb)
+    torch.cuda.synchronize()
+    nb = len(tr.reducer.buckets)
+    assert tr.reducer.launch_log == [tb] + [b for b in range(nb) if b != tb] + [("tail", tb)], tr.reducer.launch_log
+    full = tr.reducer.gather_full(tr.reducer.grad_shard) if zero1 else tr.arena.grads
+    rel = None
+    for s in tr.arena.slots:   # the reduced gradient after the step, slot by slot
+        r = rslot[s.name]
+        a, b = full[s.offset:s.offset + s.numel], ref.arena.grads[r.offset:r.offset + r.numel]
+        if s.name == "transformer.wte.weight":
+            rel = ((a - b).norm() / b.norm()).item()
+        else:
+            d = (a - b).abs().max()
+            assert d <= 1e-6 * b.abs().max() + 1e-12, (s.name, d)
+    assert 0 <= rel < 4e-3, rel   # the embedding's part rounded to bf16 once
+    rep = tr.reducer.timing_report()
+    assert rep is not None and len(rep["tied_tails"]) == 1, rep
+    print("tied bf16", "zero1" if zero1 else "allreduce", "rel", rel, "tail", rep["tied_tails"])
+print("TIED BF16 RCCL ok")
+dist.destroy_process_group()
+"""
+
+
+def test_tied_bf16_tail_on_rccl_one_rank():
+    """VERDICT r5 #5a on the real RCCL path (world-size-1 ``nccl`` group, GPT-2-tiny, gradient
+    accumulation 2): with ``tied_bf16`` the tied bucket launches first, the embedding's
+    contribution goes as a bf16 tail after every bucket, every other gradient equals the
+    no-reducer step and wte's within one bf16 rounding of the embedding part -- all-reduce
+    and ZeRO-1 (reduce-scatter) forms."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ORION_REPO=repo, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, "-c", _TIED_BF16_RCCL], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "TIED BF16 RCCL ok" in r.stdout
