@@ -9,11 +9,11 @@
 // The split recomputes S and dP once more (7 instead of 5 matmuls per (q, key) pair) but
 // each kernel keeps its accumulators and operand fragments in registers:
 //
-//   delta          delta[q] = sum_d dO O.  D = 64 (the default attn_bwd_dq4 path): written by
-//                  the dQ kernel's prologue (with the QKV bias, also the K / V bias columns),
-//                  so dQ is launched FIRST and dK/dV, which reads delta, after it on the same
-//                  stream.  D = 128 and ORION_ATTN_DQ=v3: a separate HBM-bound pass
-//                  (attn_delta_kernel) ahead of both kernels.
+//   delta          delta[q] = sum_d dO O: written by the dQ kernel's prologue (attn_bwd_dq4 at
+//                  D = 64, with the QKV bias also the K / V bias columns; attn_bwd_dq<FD> at
+//                  D = 128), so dQ is launched FIRST and dK/dV, which reads delta, after it on
+//                  the same stream.  ORION_ATTN_DQ=v3 / ORION_ATTN_DELTA=pass: a separate
+//                  HBM-bound pass (attn_delta_kernel) ahead of both kernels.
 //   kv kernel      per workgroup 32*NW keys, loop over 32-row query tiles (and the query
 //                  heads of its KV head):  S = Q K^T, dP = dO V^T (key on the lane, V
 //                  fragments in registers, K in registers or an LDS image),
@@ -489,7 +489,10 @@ __global__ __launch_bounds__(kv_waves<D>() * 64, 2) void attn_bwd_kv_kernel(Attn
 // tile advance in the scalar offset, the tile loop unrolled over the two LDS buffers (every
 // LDS address a per-lane register plus an immediate), the causal / length mask one
 // compare + select per score against a per-lane bound.
-template <int D, bool CAUSAL, bool BIAS = false>
+// FD (fused delta, round 6; the D = 128 default): delta = rowsum(dO O) is computed in the
+// prologue from this wave's own query rows and written for the dK/dV kernel, which then runs
+// AFTER this one (as attn_bwd_dq4 at D = 64) -- no separate delta pass.
+template <int D, bool CAUSAL, bool BIAS = false, bool FD = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, NCH = D / 8, TILE = BN * D, NST = BN * NCH / 256, NDB = D / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];  // [2 bufs][K|V][TILE]
@@ -521,7 +524,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams p) {
     }
     const long r = ((long)b * p.Hq + hq) * p.T + qr;
     L = p.lse[r];
-    dl = p.delta[r];
+    if constexpr (FD) {
+      const bf16_t* Or = p.o + b * p.o_sb + hq * p.o_sh + (long)qr * p.o_st;
+      float d4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const bf16x8 of = *reinterpret_cast<const bf16x8*>(Or + ks * 16 + 8 * h32);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d4[j & 3] = fmaf(bf2f(of[j]), bf2f(df[ks][j]), d4[j & 3]);
+      }
+      dl = (d4[0] + d4[1]) + (d4[2] + d4[3]);
+      dl += __shfl_xor(dl, 32);  // the other d half of the row
+      if (h32 == 0 && myq < p.T) const_cast<float*>(p.delta)[r] = dl;  // read by the dK/dV kernel
+    } else {
+      dl = p.delta[r];
+    }
   }
   const int kend = CAUSAL ? min(p.Tk, q0 + BM + off) : p.Tk;
   const int ntiles = (kend + BN - 1) / BN;
@@ -916,21 +933,32 @@ static void dq4_launch(const AttnParams& q, int grid, hipStream_t st) {
   attn_bwd_dq4_kernel<CAUSAL, BIAS><<<grid, 256, 2 * 2 * 64 * 64 * 2, st>>>(q);
 }
 
-template <int D, bool CAUSAL, bool BIAS = false>
+template <int D, bool CAUSAL, bool BIAS = false, bool FD = false>
 static void dq_launch(const AttnParams& q, int grid, hipStream_t st) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, BIAS>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, CAUSAL, BIAS, FD>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dq_lds(D));
     done = true;
   }
-  attn_bwd_dq_kernel<D, CAUSAL, BIAS><<<grid, 256, dq_lds(D), st>>>(q);
+  attn_bwd_dq_kernel<D, CAUSAL, BIAS, FD><<<grid, 256, dq_lds(D), st>>>(q);
+}
+
+// ORION_ATTN_DELTA=pass: the separate delta pass at D = 128 (A/B); default: fused into dQ
+static bool delta_pass() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORION_ATTN_DELTA");
+    v = (e && strcmp(e, "pass") == 0) ? 1 : 0;
+  }
+  return v == 1;
 }
 
 // delta (caller-allocated [B][Hq][T] fp32 scratch), dK/dV and dQ; p.dq / dk / dv are bf16
 // outputs (strided views allowed).  Order on stream st: D = 64 -- dQ (attn_bwd_dq4, writes
-// delta and the bias K / V columns), then dK/dV (reads delta); otherwise the delta pass, dK/dV,
-// dQ.
+// delta and the bias K / V columns), then dK/dV (reads delta); D = 128 -- dQ (attn_bwd_dq with
+// the fused delta), then dK/dV; ORION_ATTN_DQ=v3 / ORION_ATTN_DELTA=pass -- the delta pass,
+// dK/dV, dQ.
 int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, hipStream_t st) {
   // 32-bit buffer offsets: the dQ kernel addresses one (batch, KV head)'s K / V, the dK/dV
   // kernel one batch's Q / dO over all query heads; beyond 2 GB the caller takes the fused
@@ -1000,6 +1028,14 @@ int orion_attn_bwd_split(const AttnParams& p, int D, bool causal, float* delta, 
   dq_launch<DD, CC>(q, dq_grid, st);
   if (D == 64) {
     if (causal) { SPLIT(64, true) } else { SPLIT(64, false) }
+  } else if (D == 128 && !delta_pass()) {  // dQ first: it writes delta for dK/dV
+    if (causal) {
+      dq_launch<128, true, false, true>(q, dq_grid, st);
+      kv_launch<128, true>(q, kv_grid, st);
+    } else {
+      dq_launch<128, false, false, true>(q, dq_grid, st);
+      kv_launch<128, false>(q, kv_grid, st);
+    }
   } else if (D == 128) {
     if (causal) { SPLIT(128, true) } else { SPLIT(128, false) }
   } else {

@@ -61,6 +61,8 @@ int orion_gemm(const void*, long, const void*, long, int, int, int, int, int, vo
 int orion_gemm_colsum_scratch(int M, int N);
 int orion_gemm_lm(const void*, long, const void*, long, int, int, int, int, void*, long, float*,
                   const int64_t*, float*, const float*, const float*, hipStream_t);
+int orion_gemm_rope(const void*, long, const void*, long, int, int, int, void*, long, const float*, const float*,
+                    int, int, int, int, hipStream_t);
 int orion_lmhead_fold(const float*, int, const float*, const int64_t*, long, float*, void*, long, int, long,
                       const void*, long, const void*, long, int, float*, float*, float*, int*, int*, float*,
                       float*, int*, hipStream_t);
@@ -468,6 +470,33 @@ std::tuple<Tensor, Tensor> lmhead_bwd_prep(const Tensor& x, const Tensor& target
                                      srow.data_ptr<float>(), xs.data_ptr(), transposed ? 1 : 0, cur_stream()),
                "lmhead_bwd_prep");
   return {srow, xs};
+}
+
+// qkv (M, N) = x w^T with RoPE on the first rope_cols columns (heads of D; x (M, K) rows of
+// T tokens each, position t + pos0): Llama's packed QKV projection (csrc/gemm16.hip EPI_ROPE).
+Tensor gemm_rope(const Tensor& x, const Tensor& w, const Tensor& cos, const Tensor& sin, int64_t pos0, int64_t T,
+                 int64_t rope_cols, int64_t D) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && x.stride(-1) == 1 && x.size(-1) == w.size(1),
+              "gemm_rope: x (..., K) with unit stride, w contiguous (N, K)");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                  sin.is_contiguous() && cos.dim() == 2 && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
+              "gemm_rope: cos / sin fp32 contiguous (positions, D / 2)");
+  const int64_t K = x.size(-1), N = w.size(0);
+  auto x2 = x.reshape({-1, K});
+  const int64_t M = x2.size(0);
+  TORCH_CHECK(M % T == 0 && pos0 >= 0 && T + pos0 <= cos.size(0), "gemm_rope: rows must be whole sequences within the tables");
+  TORCH_CHECK(M < (1LL << 31) && N < (1 << 30), "gemm_rope: shape too large");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  auto out = at::empty(sizes, x.options());
+  check_launch(orion_gemm_rope(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), (int)M, (int)N, (int)K,
+                               out.data_ptr(), N, cos.data_ptr<float>(), sin.data_ptr<float>(), (int)T, (int)pos0,
+                               (int)rope_cols, (int)D, cur_stream()),
+               "gemm_rope");
+  return out;
 }
 
 // dx (N, C) = srow (.) (e . w): the LM head's input gradient from E' (N, V) and w (V, C).
@@ -1042,6 +1071,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("lmhead_fwd(Tensor x, Tensor w, Tensor targets, int ignore_index, Tensor(a!) cref) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("lmhead_bwd_prep(Tensor x, Tensor targets, int ignore_index, int V, Tensor invz, Tensor inv_n, Tensor g, bool transposed=False) -> (Tensor, Tensor)");
   m.def("gemm_rowscale(Tensor e, Tensor w, Tensor srow) -> Tensor");
+  m.def("gemm_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int pos0, int T, int rope_cols, int D) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None, bool pre_is_deriv=False) -> (Tensor, Tensor)");
   m.def("gemm_swiglu_bwd(Tensor dy, Tensor w, Tensor gate_up) -> Tensor");
@@ -1076,6 +1106,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("lmhead_fwd", &lmhead_fwd);
   m.impl("lmhead_bwd_prep", &lmhead_bwd_prep);
   m.impl("gemm_rowscale", &gemm_rowscale);
+  m.impl("gemm_rope", &gemm_rope);
   m.impl("gemm", &gemm);
   m.impl("gemm_gelu_bwd", &gemm_gelu_bwd);
   m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);

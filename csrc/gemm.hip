@@ -117,3 +117,28 @@ int orion_gemm_lm(const void* X, long ldx, const void* W, long ldw, int M, int N
   if (!gemm16_ok(a, wkm)) return -1;
   return gemm16(a, wkm, epi, st);
 }
+
+// Llama's packed QKV projection with RoPE in the epilogue (EPI_ROPE, NT W [N][K]): columns
+// [0, rcols) are heads of D = 128 rotated at position (m % T) + pos0 by the fp32 tables
+// cosv / sinv [positions][D / 2]; the rest (v) are stored as computed.
+int orion_gemm_rope(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, void* out,
+                    long ldo, const float* cosv, const float* sinv, int T, int pos0, int rcols, int D,
+                    hipStream_t st) {
+  if (M < 1 || K < 64 || K % 64 || N % 8 || N < 8) return -1;
+  if ((ldx | ldw | ldo) % 8) return -1;
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) |
+       reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(cosv) |
+       reinterpret_cast<uintptr_t>(sinv)) & 15) return -2;
+  // a wave's 128 columns are one head (D = 128: Llama's head dim); the rotated range whole waves
+  if (D != 128 || rcols % 128 || rcols > N || T < 1 || pos0 < 0 || !cosv || !sinv) return -3;
+  GemmArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)out, ldo,
+             nullptr, nullptr, 0, nullptr, 0, M, N, K, (N + 255) / 256, gemm_diag()};
+  a.rcos = cosv;
+  a.rsin = sinv;
+  a.rT = T;
+  a.rpos0 = pos0;
+  a.rcols = rcols;
+  a.rD = D;
+  if (!gemm16_ok(a, 0)) return -1;
+  return gemm16(a, 0, EPI_ROPE, st);
+}

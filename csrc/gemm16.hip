@@ -148,12 +148,49 @@ ORION_DEVICE void g16_load_bias(const GemmArgs& g, const G16Item& it, int grp, i
   }
 }
 
+// EPI_ROPE: rotate the wave's accumulators in place (before the bf16 rounding: one rounding
+// instead of the GEMM's plus the separate rope pass's).  The wave's 128 columns are aligned to
+// 128, so they hold one head of RD = 128, and column n + 64 sits in accumulator tile a + 4 of
+// the same lane and register: acc[a][b][r] is column nw + 16 a + 4 q + r of row mw + 16 b +
+// i16.  The tables are read as 16-byte rows (4 d).  (RD = 64 -- two heads per wave, partner
+// tile a + 2 -- is the same code, but instantiating both forms in one kernel spills.)
+template <int RD>
+ORION_DEVICE void g16_rope(const GemmArgs& g, f32x4 (&acc)[8][4], int mw, int q, int i16) {
+  constexpr int HB = RD / 32;  // accumulator tiles per half head
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int mc = min(mw + 16 * b + i16, g.M - 1);
+    const float* cr = g.rcos + (long)(mc % g.rT + g.rpos0) * (RD / 2) + 4 * q;
+    const float* sr = g.rsin + (long)(mc % g.rT + g.rpos0) * (RD / 2) + 4 * q;
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if ((a / HB) & 1) continue;  // second half of a head: rotated with its partner
+      const int d = (a % HB) * 16;
+      const f32x4 c = *reinterpret_cast<const f32x4*>(cr + d);
+      const f32x4 sn = *reinterpret_cast<const f32x4*>(sr + d);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x1 = acc[a][b][r], x2 = acc[a + HB][b][r];
+        acc[a][b][r] = x1 * c[r] - x2 * sn[r];
+        acc[a + HB][b][r] = x2 * c[r] + x1 * sn[r];
+      }
+    }
+    // one row's table reads in flight at a time (hoisting all 32 spills)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int EPI>
 ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16Item& it, int wm, int grp,
                                int q, int i16, u32x4 (&bias4)[4]) {
   const int m0 = it.m0, kc = it.kc, rows_m = it.rows_m;
   const int mw = m0 + wm * 64;           // this wave's 64-row block
   const int nw = it.n0 + grp * 128;      // this wave's 128 columns
+  if constexpr (EPI == EPI_ROPE) {
+    if (nw < g.rcols) {  // wave-uniform: the q | k heads
+      g16_rope<128>(g, acc, mw, q, i16);  // rD == 128 (orion_gemm_rope checks)
+    }
+  }
   if constexpr (EPI == EPI_WGRAD) {
     // fp32 partial tile into slab kc, or the final gradient (fp32 arena or bf16, scaled,
     // optionally accumulated): register quadruple = 4 consecutive n of row m
@@ -862,6 +899,7 @@ int gemm16(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
     case EPI_SWIGLU_BWD * 2 + 1: return gemm16_launch<false, true, EPI_SWIGLU_BWD>(a, st);
     case EPI_EXP * 2 + 0: return gemm16_launch<false, false, EPI_EXP>(a, st);
     case EPI_ROWSCALE * 2 + 1: return gemm16_launch<false, true, EPI_ROWSCALE>(a, st);
+    case EPI_ROPE * 2 + 0: return gemm16_launch<false, false, EPI_ROPE>(a, st);
     default: return -4;
   }
 }

@@ -7,7 +7,7 @@
 namespace orion {
 
 enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3, EPI_WGRAD = 4,
-               EPI_SWIGLU_BWD = 5, EPI_EXP = 6, EPI_ROWSCALE = 7 };
+               EPI_SWIGLU_BWD = 5, EPI_EXP = 6, EPI_ROWSCALE = 7, EPI_ROPE = 8 };
 constexpr int GEMM_DERIV = 0x100;  // orion_gemm's epi flag: GemmArgs::deriv
 
 struct GemmArgs {
@@ -42,6 +42,12 @@ struct GemmArgs {
   // GELU derivative stored instead of the pre-activation (GPT-2 MLP, round 5): EPI_BIAS_GELU
   // writes GELU'(a) as its first output, EPI_GELU_BWD multiplies by pre as given
   int deriv;
+  // EPI_ROPE (Llama's packed QKV projection, round 6): columns [0, rcols) are heads of rD = 128
+  // rotated by RoPE in the rotate-half form -- pair (d, d + rD / 2) of row m at position
+  // (m % rT) + rpos0 with the fp32 tables rcos / rsin [pos][rD / 2] -- before the bf16 store
+  const float* rcos;
+  const float* rsin;
+  int rT, rpos0, rcols, rD;
 };
 
 // ---- 16x16x32 kernel helpers (csrc/gemm16.hip)

@@ -77,8 +77,8 @@ class Attention(nn.Module):
 
     def forward(self, x, cos, sin, pos0=0):
         B, T, _ = x.shape
-        qkv = ops.linear(x, self.qkv_proj.weight).view(B, T, self.n_heads + 2 * self.n_kv, self.hd)
-        o = ops.rope_attention_packed(qkv, self.n_heads, self.n_kv, cos, sin, pos0)  # (B, T, Hq, D)
+        # (B, T, Hq, D); on the GPU with D = 128 the rotation rides in the projection's epilogue
+        o = ops.linear_rope_attention(x, self.qkv_proj.weight, self.n_heads, self.n_kv, cos, sin, pos0)
         return ops.linear(o.reshape(B, T, -1), self.o_proj.weight)
 
 

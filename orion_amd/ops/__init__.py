@@ -209,6 +209,20 @@ def rope(x, cos, sin, pos0=0):
     return ref.rope(x, cos[pos0:], sin[pos0:])
 
 
+def linear_rope_attention(x, weight, n_q, n_kv, cos, sin, pos0=0):
+    """Causal attention of (rope(q), rope(k), v) of the packed projection x W^T, W (Hq + 2 Hkv)
+    D rows -> (B, T, Hq, D).  GPU path with head dim 128: one fused node, the rotation in the
+    projection GEMM's epilogue (flash_attn.qkv_rope_flash_attention); otherwise the projection
+    then rope_attention_packed."""
+    if _gpu(x) == "hip":
+        from .flash_attn import qkv_rope_eligible, qkv_rope_flash_attention
+        if qkv_rope_eligible(x, weight, n_q, n_kv, cos):
+            return qkv_rope_flash_attention(x, weight, n_q, n_kv, cos, sin, pos0)
+    B, T, _ = x.shape
+    qkv = linear(x, weight).view(B, T, n_q + 2 * n_kv, weight.shape[0] // (n_q + 2 * n_kv))
+    return rope_attention_packed(qkv, n_q, n_kv, cos, sin, pos0)
+
+
 def rope_attention_packed(qkv, n_q, n_kv, cos, sin, pos0=0):
     """Causal attention of (rope(q), rope(k), v) on a packed (B, T, Hq + 2 Hkv, D) projection
     -> (B, T, Hq, D).  The GPU path is one fused autograd node (no per-view glue)."""
@@ -293,7 +307,8 @@ __all__ = [
     "set_backend", "backend", "ext_available", "load_ext",
     "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm",
     "token_embedding", "rope",
-    "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "cross_entropy", "swiglu_mlp",
+    "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "linear_rope_attention",
+    "cross_entropy", "swiglu_mlp",
     "linear_cross_entropy",
 ]
 
@@ -342,7 +357,7 @@ def _guarded(fn):
 
 for _name in ("layer_norm", "add_layer_norm", "add_rms_norm", "linear", "rms_norm", "bias_gelu",
               "gelu_linear", "mlp", "swiglu_mlp", "embed_layer_norm", "token_embedding", "add_broadcast",
-              "linear_attention_qkv",
+              "linear_attention_qkv", "linear_rope_attention",
               "linear_cross_entropy"):
     globals()[_name] = _guarded(globals()[_name])
 del _name

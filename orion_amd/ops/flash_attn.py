@@ -9,11 +9,13 @@ buffer, so there is no split/transpose/concat around the kernels.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from ._ext import C
 from .determinism import deterministic
+from .grad_sink import sink_of
 
 
 def _bwd_flags() -> int:
@@ -128,6 +130,63 @@ class _RopeFlashPacked(torch.autograd.Function):
                      True, scale, dqkv[:, :, :n_q], dqkv[:, :, n_q:n_q + n_kv], dqkv[:, :, n_q + n_kv:],
                      _bwd_flags(), None, cos, sin, pos0)
         return dqkv, None, None, None, None, None
+
+
+class _QKVRopeFlash(torch.autograd.Function):
+    """Llama's packed QKV projection + RoPE + causal flash attention as ONE node (round 6).
+
+    Forward: the in-tree GEMM (csrc/gemm16.hip EPI_ROPE) writes q and k already rotated -- the
+    rotation applied to the fp32 accumulators before the one bf16 rounding -- and v as computed,
+    so the separate rope pass (a read and a write of the q | k heads) is gone; the attention
+    reads the three head ranges of that buffer.  Backward: as _RopeFlashPacked, the attention
+    kernels write dq / dk un-rotated into one packed dqkv, which then feeds the projection's
+    input and weight gradients (ops/layernorm.py linear_input_weight_grads)."""
+
+    @staticmethod
+    def forward(ctx, x, w, n_q, n_kv, cos, sin, pos0):
+        B, T, _ = x.shape
+        H3 = n_q + 2 * n_kv
+        D = w.shape[0] // H3
+        qkv = C().gemm_rope(x, w, cos, sin, int(pos0), T, (n_q + n_kv) * D, D).view(B, T, H3, D)
+        scale = 1.0 / math.sqrt(D)
+        o, lse = C().attn_fwd(qkv[:, :, :n_q], qkv[:, :, n_q:n_q + n_kv], qkv[:, :, n_q + n_kv:], True, scale)
+        ctx.save_for_backward(x, w, qkv, o, lse, cos, sin)
+        ctx.meta = (n_q, n_kv, int(pos0), scale)
+        ctx.sink = sink_of(w)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        from .layernorm import linear_input_weight_grads
+        x, w, qkv, o, lse, cos, sin = ctx.saved_tensors
+        n_q, n_kv, pos0, scale = ctx.meta
+        dqkv = torch.empty_like(qkv)
+        C().attn_bwd(do.contiguous(), qkv[:, :, :n_q], qkv[:, :, n_q:n_q + n_kv], qkv[:, :, n_q + n_kv:], o, lse,
+                     True, scale, dqkv[:, :, :n_q], dqkv[:, :, n_q:n_q + n_kv], dqkv[:, :, n_q + n_kv:],
+                     _bwd_flags(), None, cos, sin, pos0)
+        dx, dw = linear_input_weight_grads(dqkv.view(-1, dqkv.shape[2] * dqkv.shape[3]), x, w, ctx.sink,
+                                           ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return dx, dw, None, None, None, None, None
+
+
+# ORION_QKV_ROPE=0: the projection on its own (hipBLASLt) and the rope pass (A/B)
+_QKV_ROPE = os.environ.get("ORION_QKV_ROPE", "1") != "0"
+
+
+def qkv_rope_eligible(x, w, n_q, n_kv, cos) -> bool:
+    from .gemm import gemm16_addressable
+    H3 = n_q + 2 * n_kv
+    if not (_QKV_ROPE and x.is_cuda and x.dim() == 3 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and w.dim() == 2 and w.shape[0] % H3 == 0 and w.shape[0] // H3 == 128 and x.stride(-1) == 1
+            and x.is_contiguous() and w.is_contiguous() and x.shape[-1] % 64 == 0 and x.data_ptr() % 16 == 0
+            and w.data_ptr() % 16 == 0 and cos.dtype == torch.float32 and cos.is_contiguous()):
+        return False
+    return gemm16_addressable(x.shape[-1], x.shape[-1], w.shape[0], False)
+
+
+def qkv_rope_flash_attention(x, w, n_q, n_kv, cos, sin, pos0=0):
+    """x (B, T, C) -> causal attention of rope(q), rope(k), v of the packed projection x w^T."""
+    return _QKVRopeFlash.apply(x, w, n_q, n_kv, cos, sin, pos0)
 
 
 def rope_flash_attention_packed(qkv, n_q, n_kv, cos, sin, pos0=0):

@@ -110,6 +110,24 @@ def add_layer_norm_hip(x, r, weight, bias, eps=1e-5, r_bias=None):
     return _AddLayerNorm.apply(x, r, weight, bias, r_bias, eps)
 
 
+def linear_input_weight_grads(dy2, x, w, sink, need_dx, need_dw):
+    """dx = dy W and dW = dy^T x of y = x W^T (dy2: (rows, N)), in the configured order
+    (ops.gemm.WGRAD_FIRST); dW goes straight into the gradient arena through ``sink`` when
+    there is one (then None is returned for it)."""
+    dx = dw = None
+    if need_dx and not WGRAD_FIRST:
+        dx = linear_dgrad(dy2, w).view(x.shape)
+    if need_dw:
+        if sink is not None:
+            wgrad_into(dy2, x.reshape(-1, x.shape[-1]), sink.view, sink.take())
+            sink.notify()
+        else:
+            dw = wgrad(dy2, x.reshape(-1, x.shape[-1]))
+    if need_dx and WGRAD_FIRST:
+        dx = linear_dgrad(dy2, w).view(x.shape)
+    return dx, dw
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T + b on hipBLASLt (or csrc/gemm.hip: ops/gemm.py); backward computes the
     bias gradient with the deterministic two-stage column-sum kernel instead of a generic
@@ -127,21 +145,12 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = dw = db = None
+        db = None
         bias_grad = ctx.has_bias and ctx.needs_input_grad[2]
         if bias_grad and WGRAD_FIRST:  # dY was just written by the previous kernel: sum it now
             db = _Linear._bias_grad(ctx, dy2)
-        if ctx.needs_input_grad[0] and not WGRAD_FIRST:
-            dx = linear_dgrad(dy2, w).view(x.shape)
-        if ctx.needs_input_grad[1]:
-            sink = ctx.sink
-            if sink is not None:
-                wgrad_into(dy2, x.reshape(-1, x.shape[-1]), sink.view, sink.take())
-                sink.notify()
-            else:
-                dw = wgrad(dy2, x.reshape(-1, x.shape[-1]))
-        if ctx.needs_input_grad[0] and WGRAD_FIRST:
-            dx = linear_dgrad(dy2, w).view(x.shape)
+        dx, dw = linear_input_weight_grads(dy2, x, w, ctx.sink, ctx.needs_input_grad[0],
+                                           ctx.needs_input_grad[1])
         if bias_grad and not WGRAD_FIRST:
             db = _Linear._bias_grad(ctx, dy2)
         return dx, dw, db

@@ -301,3 +301,38 @@ def test_gpt2_qkv_bias_grad_through_attention_matches_reference():
                           ("b", b.grad, br.grad, bb.grad)):
         assert a is not None
         within_bf16_budget(name, a, r, c)
+
+
+@pytest.mark.parametrize("B,T,Hq,Hkv,pos0", [(2, 256, 4, 2, 0), (1, 300, 2, 2, 7)])
+def test_fused_qkv_rope_attention_node(B, T, Hq, Hkv, pos0, monkeypatch):
+    """Round 6: Llama's projection + RoPE + attention as one node (the rotation in the
+    projection GEMM's epilogue, ops.linear_rope_attention) -- output and the gradients of x
+    and W against the fp32 reference (projection, rope, attention in fp32), within the budget
+    of the unfused HIP path (projection, rope pass, attention) on the same bf16 inputs."""
+    from orion_amd import ops
+    from orion_amd.ops import flash_attn as FA
+    D, Cm = 128, 256
+    g = torch.Generator(device=DEV).manual_seed(T + Hq)
+    x = (torch.randn(B, T, Cm, device=DEV, generator=g) * 0.5).bfloat16()
+    w = (torch.randn((Hq + 2 * Hkv) * D, Cm, device=DEV, generator=g) * 0.1).bfloat16()
+    do = torch.randn(B, T, Hq, D, device=DEV, generator=g).bfloat16()
+    cos, sin = ref.rope_tables(T + pos0 + 4, D, device=DEV)
+    assert FA.qkv_rope_eligible(x, w, Hq, Hkv, cos)
+
+    def run(fused):
+        monkeypatch.setattr(FA, "_QKV_ROPE", fused)
+        xx, ww = x.clone().requires_grad_(), w.clone().requires_grad_()
+        o = ops.linear_rope_attention(xx, ww, Hq, Hkv, cos, sin, pos0)
+        o.backward(do)
+        return o.detach(), xx.grad, ww.grad
+
+    got, base = run(True), run(False)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    qkv = (xr @ wr.t()).view(B, T, Hq + 2 * Hkv, D)
+    c, s = cos[pos0:pos0 + T], sin[pos0:pos0 + T]
+    q = ref.rope(qkv[:, :, :Hq], c, s)
+    k = ref.rope(qkv[:, :, Hq:Hq + Hkv], c, s)
+    o = ref.attention(q, k, qkv[:, :, Hq + Hkv:], True).float()
+    o.backward(do.float())
+    for name, a, b, cc in zip(("o", "dx", "dw"), got, (o.detach(), xr.grad, wr.grad), base):
+        within_bf16_budget(name, a, b, cc)

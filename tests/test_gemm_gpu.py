@@ -357,3 +357,37 @@ def test_per_item_walk_requests_are_reference_counted():
         r1()
         r2()
         G.set_per_item_walk(False)
+
+
+def _rope_ref(y, T, nrot, D, cos, sin, pos0):
+    """Rotate-half RoPE of the first nrot columns (heads of D) of y (M, N): row m at position
+    (m % T) + pos0 -- the fp32 reference of gemm16's EPI_ROPE."""
+    M, N = y.shape
+    y = y.clone()
+    pos = torch.arange(M, device=y.device) % T + pos0
+    c, s = cos[pos].unsqueeze(1), sin[pos].unsqueeze(1)      # (M, 1, D / 2)
+    h = y[:, :nrot].view(M, nrot // D, D)
+    x1, x2 = h[..., :D // 2].clone(), h[..., D // 2:].clone()
+    h[..., :D // 2] = x1 * c - x2 * s
+    h[..., D // 2:] = x2 * c + x1 * s
+    return y
+
+
+@pytest.mark.parametrize("B,T,K,Hq,Hkv,pos0", [(3, 100, 256, 2, 1, 5), (2, 256, 512, 4, 2, 0),
+                                               (1, 1000, 128, 3, 3, 17)])
+def test_gemm_rope_epilogue(B, T, K, Hq, Hkv, pos0, gemm_cfg):
+    """EPI_ROPE (Llama's packed QKV projection): q | k heads rotated in the epilogue at
+    position (row % T) + pos0, v heads stored as computed, ragged rows (B T not a multiple of
+    256) -- against the fp32 GEMM + rotation and the bf16 GEMM + the rope pass."""
+    from orion_amd.ops.reference import rope_tables
+    D = 128
+    g = torch.Generator(device=DEV).manual_seed(B * T + K)
+    x = _rnd(g, B * T, K)
+    w = _rnd(g, (Hq + 2 * Hkv) * D, K)
+    cos, sin = (t.to(DEV).float().contiguous() for t in rope_tables(T + pos0 + 8, D, 10000.0))
+    out = _C().gemm_rope(x, w, cos, sin, pos0, T, (Hq + Hkv) * D, D)
+    want = _rope_ref(x.float() @ w.float().t(), T, (Hq + Hkv) * D, D, cos, sin, pos0)
+    base = _rope_ref((x @ w.t()).float(), T, (Hq + Hkv) * D, D, cos, sin, pos0).bfloat16()
+    within_bf16_budget("qkv", out, want, base)
+    v0 = (Hq + Hkv) * D  # the v heads are the plain product
+    within_bf16_budget("v", out[:, v0:], want[:, v0:], (x @ w.t())[:, v0:])
