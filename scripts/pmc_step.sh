@@ -2,6 +2,7 @@
 # Whole-training-step PMC passes (each its own rocprofv3 run with --kernel-trace only):
 #   m: MFMA busy cycles, MFMA / VALU instruction counts, GPU-active cycles
 #   f: HBM-side fetch bytes (TCC FETCH_SIZE)      w: write bytes (TCC WRITE_SIZE)
+#   l (PMC_LDS=1): LDS bank conflicts / LDS-active cycles, LDS and any-dependency waits
 # over a 2-step GPT-2 bench, then the per-kernel-group table of scripts/pmc_step_summary.py.
 # usage: [PMC_PASS_TIMEOUT=seconds] scripts/pmc_step.sh TAG [bench args]
 set -o pipefail
@@ -21,7 +22,8 @@ run() {
 }
 run m SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE && \
 run f FETCH_SIZE GRBM_GUI_ACTIVE && \
-run w WRITE_SIZE GRBM_GUI_ACTIVE
+run w WRITE_SIZE GRBM_GUI_ACTIVE && \
+{ [[ -z $PMC_LDS ]] || run l SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE; }
 rc=$?
 cd "$REPO" || exit 1
 python3 scripts/pmc_step_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"

@@ -8,6 +8,10 @@ time from the kernel trace of the MFMA pass, MFMA utilisation = SQ_VALU_MFMA_BUS
 bytes and achieved bandwidth over the group's kernel time.  Counter passes come from separate
 runs of the same step; kernels are matched by dispatch order within each run.
 
+Optional pass l (PMC_LDS=1 in scripts/pmc_step.sh): LDS bank-conflict cycles per LDS-active
+cycle and the LDS / any-dependency wait share of wave cycles per group; the effective clock
+column is GRBM_GUI_ACTIVE / 8 / kernel time.
+
 usage: python scripts/pmc_step_summary.py gpurun_out/pmc_TAG
 """
 import collections
@@ -70,10 +74,10 @@ def load(d, p):
 
 def main():
     d = sys.argv[1]
-    m, f, w = load(d, "m"), load(d, "f"), load(d, "w")
+    m, f, w, lp = load(d, "m"), load(d, "f"), load(d, "w"), load(d, "l")
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     other = collections.defaultdict(float)
-    mk, fk, wk = list(m.values()), list(f.values()), list(w.values())
+    mk, fk, wk, lk = list(m.values()), list(f.values()), list(w.values()), list(lp.values())
     for i, (name, c, ns) in enumerate(mk):
         g = agg[group(name)]
         g["n"] += 1
@@ -86,14 +90,31 @@ def main():
             g["fetch"] += fk[i][1].get("FETCH_SIZE", 0.0) * 1024
         if i < len(wk) and wk[i][0] == name:
             g["write"] += wk[i][1].get("WRITE_SIZE", 0.0) * 1024
+        if i < len(lk) and lk[i][0] == name:  # optional pass l: LDS / wait counters
+            lc = lk[i][1]
+            for key in ("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS", "SQ_WAVE_CYCLES",
+                        "SQ_BUSY_CYCLES", "SQ_WAIT_ANY"):
+                g[key] += lc.get(key, 0.0)
     tot = sum(g["ns"] for g in agg.values())
     print(f"{len(mk)} dispatches, {tot / 1e6:.2f} ms of kernels (2-step bench under the counter pass)")
-    print(f"{'group':44s} {'ms':>8s} {'%':>5s} {'MFMA util':>9s} {'L2-EA GB':>8s} {'TB/s':>6s}")
+    extra = bool(lk)
+    hdr = f"{'group':44s} {'ms':>8s} {'%':>5s} {'MFMA util':>9s} {'clk GHz':>7s} {'L2-EA GB':>8s} {'TB/s':>6s}"
+    if extra:  # LDS bank-conflict cycles per LDS-active cycle; LDS / any waits per wave cycle
+        hdr += f" {'LDS conf':>8s} {'LDS wait':>8s} {'any wait':>8s}"
+    print(hdr)
     for k, g in sorted(agg.items(), key=lambda x: -x[1]["ns"]):
         util = g["mfma"] / (g["active"] / XCDS * SIMDS) if g["active"] else 0.0
+        # effective clock: GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS)
+        clk = g["active"] / XCDS / g["ns"] if g["ns"] else 0.0
         gb = (g["fetch"] + g["write"]) / 1e9
         tbs = gb / (g["ns"] / 1e9) / 1e3 if g["ns"] else 0.0
-        print(f"{k:44s} {g['ns'] / 1e6:8.2f} {100 * g['ns'] / tot:5.1f} {100 * util:8.1f}% {gb:8.2f} {tbs:6.2f}")
+        line = f"{k:44s} {g['ns'] / 1e6:8.2f} {100 * g['ns'] / tot:5.1f} {100 * util:8.1f}% {clk:7.2f} {gb:8.2f} {tbs:6.2f}"
+        if extra:
+            conf = g["SQ_LDS_BANK_CONFLICT"] / g["SQ_LDS_IDX_ACTIVE"] if g["SQ_LDS_IDX_ACTIVE"] else 0.0
+            wl = g["SQ_WAIT_INST_LDS"] / g["SQ_WAVE_CYCLES"] if g["SQ_WAVE_CYCLES"] else 0.0
+            wa = g["SQ_WAIT_ANY"] / g["SQ_WAVE_CYCLES"] if g["SQ_WAVE_CYCLES"] else 0.0
+            line += f" {100 * conf:7.1f}% {100 * wl:7.1f}% {100 * wa:7.1f}%"
+        print(line)
     print("largest kernels in 'other' (ms):")
     for k, ns in sorted(other.items(), key=lambda x: -x[1])[:8]:
         print(f"  {k:70s} {ns / 1e6:8.2f}")
