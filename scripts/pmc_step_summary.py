@@ -108,7 +108,8 @@ def main():
         clk = g["active"] / XCDS / g["ns"] if g["ns"] else 0.0
         gb = (g["fetch"] + g["write"]) / 1e9
         tbs = gb / (g["ns"] / 1e9) / 1e3 if g["ns"] else 0.0
-        line = f"{k:44s} {g['ns'] / 1e6:8.2f} {100 * g['ns'] / tot:5.1f} {100 * util:8.1f}% {clk:7.2f} {gb:8.2f} {tbs:6.2f}"
+        line = (f"{k:44s} {g['ns'] / 1e6:8.2f} {100 * g['ns'] / tot:5.1f} {100 * util:8.1f}% {clk:7.2f} "
+                f"{gb:8.2f} {tbs:6.2f}")
         if extra:
             conf = g["SQ_LDS_BANK_CONFLICT"] / g["SQ_LDS_IDX_ACTIVE"] if g["SQ_LDS_IDX_ACTIVE"] else 0.0
             wl = g["SQ_WAIT_INST_LDS"] / g["SQ_WAVE_CYCLES"] if g["SQ_WAVE_CYCLES"] else 0.0

@@ -65,10 +65,29 @@ def test_pmc_step_summary_utilisation_and_traffic(tmp_path):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     gemm = [ln for ln in r.stdout.splitlines() if ln.startswith("GEMM hipBLASLt")][0].split()
-    # 50 % MFMA busy by construction; 2 KiB per ns of kernel time = 2.048 TB/s
-    assert gemm[-3] == "50.0%"
+    # 50 % MFMA busy by construction at a 2.0 GHz effective clock (GRBM_GUI_ACTIVE / 8 / ns);
+    # 2 KiB per ns of kernel time = 2.048 TB/s
+    assert gemm[-4] == "50.0%"
+    assert gemm[-3] == "2.00"
     assert gemm[-2] == f"{2 * 1024 * 600_000 / 1e9:.2f}"
     assert gemm[-1] == "2.05"
+    # the optional LDS pass: conflict cycles per LDS-active cycle, LDS / any waits per wave cycle
+    d = tmp_path / "l"
+    d.mkdir()
+    _trace(d / "run_kernel_trace.csv", kernels)
+    with open(d / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for i, (name, _, ns) in enumerate(kernels):
+            for cn, cv in (("SQ_LDS_BANK_CONFLICT", 1.0 * ns), ("SQ_LDS_IDX_ACTIVE", 4.0 * ns),
+                           ("SQ_WAIT_INST_LDS", 1.0 * ns), ("SQ_WAIT_ANY", 3.0 * ns),
+                           ("SQ_WAVE_CYCLES", 10.0 * ns)):
+                w.writerow(dict(Dispatch_Id=i + 1, Kernel_Name=name, Counter_Name=cn, Counter_Value=cv))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_step_summary.py"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    gemm = [ln for ln in r.stdout.splitlines() if ln.startswith("GEMM hipBLASLt")][0].split()
+    assert gemm[-3:] == ["25.0%", "10.0%", "30.0%"], gemm
 
 
 def test_pmc_step_summary_groups_gemm16_by_epilogue():
