@@ -63,6 +63,7 @@ int orion_gemm_lm(const void*, long, const void*, long, int, int, int, int, void
                   const int64_t*, float*, const float*, const float*, hipStream_t);
 int orion_gemm_rope(const void*, long, const void*, long, int, int, int, void*, long, const float*, const float*,
                     int, int, int, int, hipStream_t);
+int orion_gemm_swiglu(const void*, long, const void*, long, int, int, int, void*, long, void*, long, hipStream_t);
 int orion_lmhead_fold(const float*, int, const float*, const int64_t*, long, float*, void*, long, int, long,
                       const void*, long, const void*, long, int, float*, float*, float*, int*, int*, float*,
                       float*, int*, hipStream_t);
@@ -497,6 +498,24 @@ Tensor gemm_rope(const Tensor& x, const Tensor& w, const Tensor& cos, const Tens
                                (int)rope_cols, (int)D, cur_stream()),
                "gemm_rope");
   return out;
+}
+
+// (gu (M, 2F), h (M, F)) = (x w^T, silu(gate) * up) for w = [W_gate; W_up] (2F, K): Llama's
+// gate_up projection with the SwiGLU forward in the epilogue (csrc/gemm16.hip EPI_SWIGLU).
+std::vector<Tensor> gemm_swiglu(const Tensor& x, const Tensor& w) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && x.dim() == 2 && x.stride(1) == 1 && x.size(1) == w.size(1),
+              "gemm_swiglu: x (M, K) with unit stride, w contiguous (2F, K)");
+  const int64_t M = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  TORCH_CHECK(w.size(0) % 256 == 0 && M < (1LL << 31) && F < (1 << 29), "gemm_swiglu: 2F % 256 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto gu = at::empty({M, 2 * F}, x.options());
+  auto h = at::empty({M, F}, x.options());
+  check_launch(orion_gemm_swiglu(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), (int)M, (int)F, (int)K,
+                                 gu.data_ptr(), 2 * F, h.data_ptr(), F, cur_stream()),
+               "gemm_swiglu");
+  return {gu, h};
 }
 
 // dx (N, C) = srow (.) (e . w): the LM head's input gradient from E' (N, V) and w (V, C).
@@ -1072,6 +1091,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("lmhead_bwd_prep(Tensor x, Tensor targets, int ignore_index, int V, Tensor invz, Tensor inv_n, Tensor g, bool transposed=False) -> (Tensor, Tensor)");
   m.def("gemm_rowscale(Tensor e, Tensor w, Tensor srow) -> Tensor");
   m.def("gemm_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int pos0, int T, int rope_cols, int D) -> Tensor");
+  m.def("gemm_swiglu(Tensor x, Tensor w) -> Tensor[]");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None, bool pre_is_deriv=False) -> (Tensor, Tensor)");
   m.def("gemm_swiglu_bwd(Tensor dy, Tensor w, Tensor gate_up) -> Tensor");
@@ -1107,6 +1127,7 @@ TORCH_LIBRARY_IMPL(orion_amd, CUDA, m) {
   m.impl("lmhead_bwd_prep", &lmhead_bwd_prep);
   m.impl("gemm_rowscale", &gemm_rowscale);
   m.impl("gemm_rope", &gemm_rope);
+  m.impl("gemm_swiglu", &gemm_swiglu);
   m.impl("gemm", &gemm);
   m.impl("gemm_gelu_bwd", &gemm_gelu_bwd);
   m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);

@@ -13,6 +13,7 @@
 //                  per-64-row column sums of out (the fc bias gradient)
 //   EPI_SWIGLU_BWD out = acc * up * silu'(gate), out2 = acc * silu(gate)     (Llama down_proj
 //                  with gate = pre[m][n], up = pre[m][N + n]                   dgrad)
+//   EPI_SWIGLU     out = [gate | up] = X [W_g; W_u]^T, out2 = silu(gate) up   (Llama gate_up)
 // The last two remove the separate bias+GELU forward and GELU backward HBM passes over the
 // (tokens x 4C) activation.
 //
@@ -141,4 +142,21 @@ int orion_gemm_rope(const void* X, long ldx, const void* W, long ldw, int M, int
   a.rD = D;
   if (!gemm16_ok(a, 0)) return -1;
   return gemm16(a, 0, EPI_ROPE, st);
+}
+
+// Llama's gate_up projection with SwiGLU in the epilogue (EPI_SWIGLU, NT W = [W_gate; W_up]
+// [2F][K]): gu [M][2F] (kept for the backward) and h = silu(gate) * up [M][F].  F % 128 == 0
+// (a wave's 128 tile columns are 64 gate + 64 up features); the whole W within 32-bit offsets.
+int orion_gemm_swiglu(const void* X, long ldx, const void* W, long ldw, int M, int F, int K, void* gu,
+                      long ldg, void* h, long ldh, hipStream_t st) {
+  if (M < 1 || K < 64 || K % 64 || F < 128 || F % 128) return -1;
+  if ((ldx | ldw | ldg | ldh) % 8) return -1;
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(gu) |
+       reinterpret_cast<uintptr_t>(h)) & 15) return -2;
+  const int N = 2 * F;
+  if ((long)N * ldw * 2 >= 0xFFFFFF00L) return -1;
+  GemmArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)gu, ldg,
+             nullptr, (bf16_t*)h, ldh, nullptr, 0, M, N, K, N / 256, gemm_diag()};
+  if (!gemm16_ok(a, 0)) return -1;
+  return gemm16(a, 0, EPI_SWIGLU, st);
 }

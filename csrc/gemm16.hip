@@ -229,8 +229,18 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
   const __amdgpu_buffer_rsrc_t ro =
       make_rsrc(g.out + (long)m0 * g.ldo, (unsigned)(((long)(rows_m - 1) * g.ldo + g.N) * 2));
   [[maybe_unused]] __amdgpu_buffer_rsrc_t ro2 = ro;
-  if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD)
-    ro2 = make_rsrc(g.out2 + (long)m0 * g.ldo2, (unsigned)(((long)(rows_m - 1) * g.ldo2 + g.N) * 2));
+  // a second output: GELU activation, SwiGLU' dup, SwiGLU h (written by the up half, ap 2 / 3)
+  constexpr bool TWO = EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD || EPI == EPI_SWIGLU;
+  if constexpr (TWO)
+    ro2 = make_rsrc(g.out2 + (long)m0 * g.ldo2,
+                    (unsigned)(((long)(rows_m - 1) * g.ldo2 + (EPI == EPI_SWIGLU ? g.N >> 1 : g.N)) * 2));
+  // EPI_SWIGLU: tile column c of the wave -> output column (gate f, or up F + f) and h column f
+  auto ocol = [&](int c) {
+    if constexpr (EPI != EPI_SWIGLU) return c;
+    const int off = c - nw;
+    return (nw >> 1) + off + (off >= 64 ? (g.N >> 1) - 64 : 0);
+  };
+  auto ocol2 = [&](int c) { return EPI == EPI_SWIGLU ? (nw >> 1) + c - nw - 64 : c; };
   constexpr bool CS = EPI == EPI_GELU_BWD;
   // bf16 pair word -> two floats (low half first)
   auto unpack2 = [](unsigned w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)}; };
@@ -354,6 +364,21 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
         for (int e = 0; e < 4; ++e) v[e] *= splat2(rsb[b]);
       }
       [[maybe_unused]] f32x2 du[4];
+      if constexpr (EPI == EPI_SWIGLU) {
+        // up half: h = silu(gate) up, the gate of the same columns from tiles 2 (ap - 2) (+ 1)
+        if (ap >= 2) {
+          f32x2 vg[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * ap - 4][b][r]),
+                                                             __float_as_uint(acc[2 * ap - 3][b][r]), false, false);
+            vg[r >> 1][r & 1] = __uint_as_float(sw[0]);
+            vg[2 + (r >> 1)][r & 1] = __uint_as_float(sw[1]);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) du[e] = vg[e] * sigmoid2(vg[e]) * v[e];
+        }
+      }
       if constexpr (EPI == EPI_SWIGLU_BWD) {
         // v = dh; dgate = dh u silu'(g), dup = dh silu(g)
 #pragma unroll
@@ -376,11 +401,13 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) pk[e] = pack2_bf16(v[e]);
-        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
+        if constexpr (TWO) {
+          if (EPI != EPI_SWIGLU || ap >= 2) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if constexpr (EPI == EPI_BIAS_GELU) pk2[e] = pack2_bf16(G16_DIAG_GELU ? gelu_x2(v[e]) : v[e] * v[e]);
-            else pk2[e] = pack2_bf16(du[e]);
+            for (int e = 0; e < 4; ++e) {
+              if constexpr (EPI == EPI_BIAS_GELU) pk2[e] = pack2_bf16(G16_DIAG_GELU ? gelu_x2(v[e]) : v[e] * v[e]);
+              else pk2[e] = pack2_bf16(du[e]);
+            }
           }
         }
       }
@@ -393,7 +420,9 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
         // each over both pairs' 32 + 32 columns (8 rows x 128 B)
         if ((ap & 1) == 0) {
           parkA[b] = pk;
-          if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) parkB[b] = pk2;
+          if constexpr (TWO) {
+            if (EPI != EPI_SWIGLU || ap >= 2) parkB[b] = pk2;
+          }
         } else {
           const int hi = (i16 >> 3) & 1;
           auto xchg = [&](const u32x4& a, const u32x4& bb, u32x4& n0, u32x4& n1) {
@@ -411,14 +440,16 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
           const int ncx = nw + 16 * (2 * (ap - 1 + hi) + (q & 1)) + 8 * (q >> 1);
           const int mr0 = mw + 16 * b + (i16 & 7), mr1 = mr0 + 8;
           const bool nx = ncx < g.N;
-          const unsigned o0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo + ncx) * 2) : 0xFFFFFFF0u;
-          const unsigned o1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo + ncx) * 2) : 0xFFFFFFF0u;
+          const int oc = ocol(ncx);
+          const unsigned o0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo + oc) * 2) : 0xFFFFFFF0u;
+          const unsigned o1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo + oc) * 2) : 0xFFFFFFF0u;
           __builtin_amdgcn_raw_buffer_store_b128(n0, ro, o0, 0, AUX1);
           __builtin_amdgcn_raw_buffer_store_b128(n1, ro, o1, 0, AUX1);
-          if constexpr ((EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) && G16_DIAG_ST2) {
+          if (TWO && G16_DIAG_ST2 && (EPI != EPI_SWIGLU || ap == 3)) {
             xchg(parkB[b], pk2, n0, n1);
-            unsigned p0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
-            unsigned p1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo2 + ncx) * 2) : 0xFFFFFFF0u;
+            const int oc2 = ocol2(ncx);
+            unsigned p0 = (mr0 < g.M && nx) ? (unsigned)(((long)(mr0 - m0) * g.ldo2 + oc2) * 2) : 0xFFFFFFF0u;
+            unsigned p1 = (mr1 < g.M && nx) ? (unsigned)(((long)(mr1 - m0) * g.ldo2 + oc2) * 2) : 0xFFFFFFF0u;
 #if G16_DIAG_ST2_SMALL  // diagnostic: the second output folded into its first 256 KB (L2-resident)
             p0 &= 0x3FFF0u;
             p1 &= 0x3FFF0u;
@@ -429,10 +460,10 @@ ORION_DEVICE void g16_epilogue(const GemmArgs& g, f32x4 (&acc)[8][4], const G16I
         }
       } else {
         const bool ok = m < g.M && nok;
-        const unsigned off = ok ? (unsigned)(((long)(m - m0) * g.ldo + nb) * 2) : 0xFFFFFFF0u;
+        const unsigned off = ok ? (unsigned)(((long)(m - m0) * g.ldo + ocol(nb)) * 2) : 0xFFFFFFF0u;
         __builtin_amdgcn_raw_buffer_store_b128(pk, ro, off, 0, AUX1);
-        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) {
-          const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + nb) * 2) : 0xFFFFFFF0u;
+        if (TWO && (EPI != EPI_SWIGLU || ap >= 2)) {
+          const unsigned off2 = ok ? (unsigned)(((long)(m - m0) * g.ldo2 + ocol2(nb)) * 2) : 0xFFFFFFF0u;
           __builtin_amdgcn_raw_buffer_store_b128(pk2, ro2, off2, 0, G16_ST2_AUX);
         }
       }
@@ -571,6 +602,8 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   auto setup_w = [&](const G16Item& it) {
     if constexpr (WKM)
       rw = make_rsrc(g.W + (long)it.k0 * g.ldw + it.n0, (unsigned)(((long)(it.kr - 1) * g.ldw + it.rows_n) * 2));
+    else if constexpr (EPI == EPI_SWIGLU)  // gate and up rows F apart: the whole W (orion_gemm_swiglu checks)
+      rw = make_rsrc(g.W + it.k0, (unsigned)(((long)(g.N - 1) * g.ldw + it.kr) * 2));
     else
       rw = make_rsrc(g.W + (long)it.n0 * g.ldw + it.k0, (unsigned)(((long)(it.rows_n - 1) * g.ldw + it.kr) * 2));
 #pragma unroll
@@ -586,7 +619,12 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
         } else {  // [256 n][64 k]: rows grp 128 + hh 64 + [0, 64)
           const int row0 = grp * 128 + hh * 64 + b * 8, row = row0 + lr;
           const int ch = slot ^ nt_swz(row);
-          vo[p][e] = (unsigned)(((long)(min(it.n0 + row, g.N - 1) - it.n0) * g.ldw + 8 * ch) * 2);
+          if constexpr (EPI == EPI_SWIGLU) {  // image row -> gate row f (hh 0) / up row F + f (hh 1)
+            const int f = ((it.n0 + grp * 128) >> 1) + b * 8 + lr;
+            vo[p][e] = (unsigned)(((long)(f + hh * (g.N >> 1)) * g.ldw + 8 * ch) * 2);
+          } else {
+            vo[p][e] = (unsigned)(((long)(min(it.n0 + row, g.N - 1) - it.n0) * g.ldw + 8 * ch) * 2);
+          }
         }
       }
     }
@@ -723,7 +761,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(GemmArgs g) {
   // streams' pieces, then vmcnt(<this phase's own loads>), so every older piece has landed
   // before the next phase), MMA slot (32 MFMAs)
   // stores a wave issues in every non-WGRAD epilogue (at least): G16_DEFER's wait count
-  constexpr int NST = ((EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) && G16_DIAG_ST2) ? 32 : 16;
+  constexpr int NST = !G16_DIAG_ST2 ? 16 : (EPI == EPI_BIAS_GELU || EPI == EPI_SWIGLU_BWD) ? 32 : EPI == EPI_SWIGLU ? 24 : 16;
   [[maybe_unused]] u32x4 bias4[4];
   // tail: the item's last phase; its closing barrier is left to the caller (G16_EPI_SYNC)
   auto phase = [&](auto Hc, int s, int t, bool defer, bool tail) {
@@ -900,6 +938,7 @@ int gemm16(const GemmArgs& a0, int wkm, int epi, hipStream_t st) {
     case EPI_EXP * 2 + 0: return gemm16_launch<false, false, EPI_EXP>(a, st);
     case EPI_ROWSCALE * 2 + 1: return gemm16_launch<false, true, EPI_ROWSCALE>(a, st);
     case EPI_ROPE * 2 + 0: return gemm16_launch<false, false, EPI_ROPE>(a, st);
+    case EPI_SWIGLU * 2 + 0: return gemm16_launch<false, false, EPI_SWIGLU>(a, st);
     default: return -4;
   }
 }

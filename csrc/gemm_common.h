@@ -7,7 +7,8 @@
 namespace orion {
 
 enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_GELU_BWD = 3, EPI_WGRAD = 4,
-               EPI_SWIGLU_BWD = 5, EPI_EXP = 6, EPI_ROWSCALE = 7, EPI_ROPE = 8 };
+               EPI_SWIGLU_BWD = 5, EPI_EXP = 6, EPI_ROWSCALE = 7, EPI_ROPE = 8,
+               EPI_SWIGLU = 9 };
 constexpr int GEMM_DERIV = 0x100;  // orion_gemm's epi flag: GemmArgs::deriv
 
 struct GemmArgs {
@@ -48,6 +49,11 @@ struct GemmArgs {
   const float* rcos;
   const float* rsin;
   int rT, rpos0, rcols, rD;
+  // EPI_SWIGLU (Llama's gate_up projection, round 6): N = 2F, W = [W_gate; W_up] [2F][K].  The
+  // wave owning tile columns [nw, nw + 128) computes gate features f = nw / 2 + [0, 64) in its
+  // first 64 columns and the matching up rows F + f in the last 64 (the W stream reads those
+  // rows), so silu(gate) * up is lane-local: out = the packed gate | up projection [M][2F] in
+  // its natural layout, out2 = h [M][F]
 };
 
 // ---- 16x16x32 kernel helpers (csrc/gemm16.hip)

@@ -247,6 +247,12 @@ _FUSED_SWIGLU = os.environ.get("ORION_FUSED_SWIGLU", "1") != "0"
 # so the default stays 0
 _SWIGLU_BWD_ORDER = os.environ.get("ORION_SWIGLU_BWD_ORDER", "0")
 
+# ORION_SWIGLU_FWD=gemm (default): the gate_up projection runs on gemm16 with the SwiGLU forward
+# in its epilogue (csrc/gemm16.hip EPI_SWIGLU; needs F % 128 == 0): one kernel writes gu and
+# h, the separate swiglu_fwd pass over (M, 2F) is gone.  =pass: hipBLASLt
+# gate_up + the swiglu_fwd pass.
+_SWIGLU_FWD = os.environ.get("ORION_SWIGLU_FWD", "gemm")
+
 
 def swiglu_mlp_ok(x, w_gu, w_down) -> bool:
     from .gemm import gemm16_addressable
@@ -264,7 +270,8 @@ class _SwigluMLP(torch.autograd.Function):
     """y = (silu(x W_g^T) * (x W_u^T)) W_down^T with W_gu = [W_g; W_u] packed, Llama's
     feed-forward.
 
-    forward   gu = x W_gu^T (hipBLASLt), h = swiglu(gu) (csrc/activations.hip), y = h W_down^T;
+    forward   (gu, h) = ONE in-tree GEMM x W_gu^T with h = silu(gate) * up in its epilogue
+              (_SWIGLU_FWD; else hipBLASLt + the swiglu pass), y = h W_down^T;
     backward  dgu = ONE in-tree GEMM dy W_down whose epilogue reads gate / up from gu and
               writes dgate = dh up silu'(gate), dup = dh silu(gate) straight into the packed
               (M, 2F) gradient; dW_down = dy^T h, dx = dgu W_gu, dW_gu = dgu^T x (weight
@@ -274,8 +281,11 @@ class _SwigluMLP(torch.autograd.Function):
     def forward(ctx, x, w_gu, w_down):
         C_ = x.shape[-1]
         x2 = x.reshape(-1, C_)
-        gu = linear_fwd(x2, w_gu)
-        h = C().swiglu_fwd(gu)
+        if _SWIGLU_FWD == "gemm" and w_gu.shape[0] % 256 == 0 and w_gu.numel() * 2 < 0xFFFFFF00:
+            gu, h = C().gemm_swiglu(x2, w_gu)
+        else:
+            gu = linear_fwd(x2, w_gu)
+            h = C().swiglu_fwd(gu)
         y = linear_fwd(h, w_down)
         ctx.save_for_backward(x2, gu, h, w_gu, w_down)
         ctx.sinks = (sink_of(w_gu), sink_of(w_down))

@@ -295,13 +295,15 @@ def test_gemm_swiglu_bwd_epilogue(M, C_, F_, gemm_cfg):
     within_bf16_budget("dup", got[:, F_:], gr.grad[:, F_:], gb.grad[:, F_:])
 
 
-def test_swiglu_mlp_matches_reference():
+@pytest.mark.parametrize("F_", [1376, 1408])
+def test_swiglu_mlp_matches_reference(F_):
     """ops.swiglu_mlp (Llama feed-forward, SwiGLU backward fused into the down_proj input
-    gradient GEMM) against fp32 autograd: output and every gradient, ragged token count."""
+    gradient GEMM; F = 1408 also the SwiGLU forward in the gate_up GEMM's epilogue, 1376 the
+    swiglu pass) against fp32 autograd: output and every gradient, ragged token count."""
     from orion_amd import ops
     g = torch.Generator(device=DEV).manual_seed(9)
     x = _rnd(g, 3, 111, 512)
-    wgu, wd = _rnd(g, 2 * 1376, 512) * 0.1, _rnd(g, 512, 1376) * 0.05
+    wgu, wd = _rnd(g, 2 * F_, 512) * 0.1, _rnd(g, 512, F_) * 0.05
     dy = _rnd(g, 3, 111, 512)
     ts = [t.clone().requires_grad_() for t in (x, wgu, wd)]
     y = ops.swiglu_mlp(*ts)
@@ -357,6 +359,23 @@ def test_per_item_walk_requests_are_reference_counted():
         r1()
         r2()
         G.set_per_item_walk(False)
+
+
+@pytest.mark.parametrize("M,K,F_", [(300, 256, 128), (513, 512, 384), (2048, 128, 640), (4096, 768, 1408)])
+def test_gemm_swiglu_epilogue(M, K, F_, gemm_cfg):
+    """EPI_SWIGLU (Llama's gate_up projection): the W stream reads gate rows f and up rows F + f
+    into one wave's tile, the epilogue writes gu in its natural (M, 2F) layout and h = silu(gate)
+    up -- against the fp32 GEMM + SwiGLU and the bf16 GEMM + the swiglu pass, ragged M."""
+    g = torch.Generator(device=DEV).manual_seed(M + K + F_)
+    x = _rnd(g, M, K)
+    w = _rnd(g, 2 * F_, K)
+    gu, h = _C().gemm_swiglu(x, w)
+    want = x.float() @ w.float().t()
+    base = x @ w.t()
+    within_bf16_budget("gu", gu, want, base)
+    assert gu.shape == (M, 2 * F_) and h.shape == (M, F_)
+    ga, ua = want.chunk(2, -1)
+    within_bf16_budget("h", h, torch.nn.functional.silu(ga) * ua, _C().swiglu_fwd(base))
 
 
 def _rope_ref(y, T, nrot, D, cos, sin, pos0):
