@@ -60,10 +60,14 @@ class FlatAdamW:
         """Fill the device hyper-parameter vector for the NEXT step (host -> device)."""
         t = self.step_count + 1
         b1, b2 = self.betas
+        # pinned + non_blocking: a pageable copy would make the host wait for the whole
+        # backward before it launched the optimizer (a ~40 us idle gap per step in the kernel
+        # trace); the caching host allocator keeps the pinned block until its copy has run
         vals = torch.tensor([self.lr, b1, b2, self.eps, self.weight_decay,
                              1.0 - b1 ** t, 1.0 - b2 ** t,
-                             self.grad_clip if self.grad_clip else 0.0], dtype=torch.float32)
-        self._hyper.copy_(vals, non_blocking=False)
+                             self.grad_clip if self.grad_clip else 0.0], dtype=torch.float32,
+                            pin_memory=self._use_hip)
+        self._hyper.copy_(vals, non_blocking=self._use_hip)
         return self._hyper
 
     # ------------------------------------------------------------------ step
