@@ -390,12 +390,62 @@ __global__ __launch_bounds__(256) void colsum3_stage2_kernel(const float* __rest
   store_grad(out, c, s, o.f32);
 }
 
+// One-pass form (round 6, the default): workgroup (column block, z) folds ALL P rows of its
+// CW columns -- lane = (row 64 / CW sub-row, column), NW waves, wave w rows (w + NW k) 64 / CW +
+// sub with 16 loads in flight per lane, then the NW x 64 / CW partial sums in a fixed order --
+// so the two ~5 us launches of the two-stage form become one (the partials were just written:
+// they are read from the caches).  Narrow column blocks give the launch enough workgroups
+// (C = 768: 48 per output).  Deterministic.
+template <int NW, int CW>
+__global__ __launch_bounds__(NW * 64) void colsum_onepass_kernel(const float* __restrict__ part, long zstride,
+                                                                 int P, int C, ColsumOuts o) {
+  constexpr int R = 64 / CW;  // rows per wave load
+  void* out = o.out[blockIdx.y];
+  if (!out) return;  // block-uniform, before the barrier
+  __shared__ float red[NW * R][CW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sub = lane / CW, cl = lane % CW;
+  const int c = blockIdx.x * CW + cl;
+  const float* pz = part + blockIdx.y * zstride;
+  float s = 0.f;
+  if (c < C) {
+    // 16 predicated loads in flight per lane: P <= 1024 rows is ONE round trip per lane
+    constexpr int STEP = NW * R, U = 16;
+    for (int p = wv * R + sub; p < P; p += U * STEP) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = p + u * STEP < P ? pz[(size_t)(p + u * STEP) * C + c] : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += v[u];
+    }
+  }
+  red[wv * R + sub][cl] = s;
+  __syncthreads();
+  if (threadIdx.x < CW && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW * R; ++w) t += red[w][cl];
+    store_grad(out, c, t, o.f32);
+  }
+}
+
 }  // namespace orion
 
 using namespace orion;
 
 int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, int f32,
                            hipStream_t st);
+
+// ORION_COLSUM=2: the two-stage column sums (A/B); default one pass
+static bool colsum_two_stage() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORION_COLSUM");
+    v = (e && e[0] == '2') ? 1 : 0;
+  }
+  return v == 1;
+}
+constexpr int COLSUM_NW = 16, COLSUM_CW = 16;
 
 // exact_fit: 4-wide slices when they tile the row exactly and 8-wide ones would not
 // (C = 768: 3 x 64 x 4 uses every lane, 2 x 64 x 8 leaves a third idle).  Measured on
@@ -536,9 +586,13 @@ int orion_layernorm_bwd(const void* dy, const void* x, const void* w, const floa
   float* mid = part + 3 * (size_t)nb * C;
   if (dw || db || drbias) {
     const ColsumOuts o{{dw, db, drbias}, grad_f32};
-    const int rps = (nb + COLSUM_SPLITS - 1) / COLSUM_SPLITS;
-    colsum3_stage1_kernel<<<dim3((C + 63) / 64, COLSUM_SPLITS, 3), 256, 0, st>>>(part, mid, nb, C, rps, o);
-    colsum3_stage2_kernel<<<dim3((C + 255) / 256, 3), 256, 0, st>>>(mid, COLSUM_SPLITS, C, o);
+    if (!colsum_two_stage()) {
+      colsum_onepass_kernel<COLSUM_NW, COLSUM_CW><<<dim3((C + COLSUM_CW - 1) / COLSUM_CW, 3), COLSUM_NW * 64, 0, st>>>(part, (long)nb * C, nb, C, o);
+    } else {
+      const int rps = (nb + COLSUM_SPLITS - 1) / COLSUM_SPLITS;
+      colsum3_stage1_kernel<<<dim3((C + 63) / 64, COLSUM_SPLITS, 3), 256, 0, st>>>(part, mid, nb, C, rps, o);
+      colsum3_stage2_kernel<<<dim3((C + 255) / 256, 3), 256, 0, st>>>(mid, COLSUM_SPLITS, C, o);
+    }
   }
   return (int)hipGetLastError();
 }
@@ -585,6 +639,11 @@ int orion_colsum_bf16(const void* m, void* out, float* part, int rows, int C, in
 // part[P][C] partials; mid: COLSUM_SPLITS * C floats of scratch; out fp32 when f32
 int orion_colsum_partials2(const float* part, float* mid, void* out, int P, int C, int f32,
                            hipStream_t st) {
+  if (!colsum_two_stage()) {
+    const ColsumOuts o{{out, nullptr, nullptr}, f32};
+    colsum_onepass_kernel<COLSUM_NW, COLSUM_CW><<<dim3((C + COLSUM_CW - 1) / COLSUM_CW, 1), COLSUM_NW * 64, 0, st>>>(part, 0, P, C, o);
+    return (int)hipGetLastError();
+  }
   const int S = P < COLSUM_SPLITS ? (P < 1 ? 1 : P) : COLSUM_SPLITS;
   const int rps = (P + S - 1) / S;
   colsum_stage1_kernel<<<dim3((C + 63) / 64, S), 256, 0, st>>>(part, mid, P, C, rps);
