@@ -36,6 +36,13 @@ def group(name):
         return "GEMM gemm16 fwd + bias + GELU epilogue"
     if "gemm16_kernel<false, true, 5" in n:
         return "GEMM gemm16 dgrad + SwiGLU' epilogue"
+    for key, g in (("gemm16_kernel<true, false, 4", "GEMM gemm16 weight gradients (NT operand)"),
+                   ("gemm16_kernel<false, false, 6", "GEMM gemm16 LM-head fwd + exp epilogue"),
+                   ("gemm16_kernel<false, true, 7", "GEMM gemm16 LM-head dgrad (row-scaled)"),
+                   ("gemm16_kernel<false, false, 8", "GEMM gemm16 fwd + RoPE epilogue"),
+                   ("gemm16_kernel<false, false, 9", "GEMM gemm16 fwd + SwiGLU epilogue")):
+        if key in n:
+            return g
     if "gemm16_kernel" in n:
         return "GEMM gemm16 input gradients"
     if "cijk" in n or "gemm[" in n:

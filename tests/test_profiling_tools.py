@@ -100,3 +100,7 @@ def test_pmc_step_summary_groups_gemm16_by_epilogue():
     assert g("void orion::gemm16_kernel<false, true, 0, false>(orion::GemmArgs)") == "GEMM gemm16 input gradients"
     assert g("Custom_Cijk_Alik_Bljk_BBS_BH_MT256x256x64") == "GEMM hipBLASLt (forward)"
     assert g("void orion::attn_bwd_kv_kernel<64, true, false>(orion::AttnParams)") == "attention bwd dK/dV"
+    assert "SwiGLU epilogue" in g("void orion::gemm16_kernel<false, false, 9, false>(orion::GemmArgs)")
+    assert "RoPE" in g("void orion::gemm16_kernel<false, false, 8, false>(orion::GemmArgs)")
+    assert "exp epilogue" in g("void orion::gemm16_kernel<false, false, 6, false>(orion::GemmArgs)")
+    assert "NT operand" in g("void orion::gemm16_kernel<true, false, 4, false>(orion::GemmArgs)")
