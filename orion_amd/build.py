@@ -2,8 +2,9 @@
 
 No hipify, no JIT cache, no setuptools magic: every ``csrc/*.hip`` kernel file
 is compiled by ``hipcc --offload-arch=gfx950`` into an object with no torch
-headers (fast, pure kernel code), ``csrc/bindings.cpp`` is compiled against
-the torch headers, and everything is linked into one shared object that
+headers (fast, pure kernel code), the host sources ``csrc/*.cpp`` (the op
+bindings, the hipBLASLt wrapper) are compiled against the torch headers, and
+everything is linked into one shared object that
 registers ``torch.ops.orion_amd.*`` on load.  Objects are rebuilt only when a
 source or header is newer than the object.
 
@@ -76,7 +77,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
             "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H"]
     jobs_list = []
     objs = []
-    for src in sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + [os.path.join(CSRC, "bindings.cpp")]:
+    for src in sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         base = bind if src.endswith(".cpp") else kern
@@ -112,7 +113,8 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     if force or jobs_list or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest_obj:
         tlib = libdirs[0]
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp",
-                f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+                # hipBLASLt: the copy torch ships and loads (csrc/blaslt.cpp)
+                f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lhipblaslt",
                 f"-Wl,-rpath,{tlib}"]
         _run(link, verbose)
         os.replace(OUT + ".tmp", OUT)

@@ -73,10 +73,13 @@ class CausalSelfAttention(nn.Module):
         self.n_head = cfg.n_head
         self.dropout = cfg.dropout
 
+    def attend(self, x):
+        """QKV projection + attention, before the output projection (B, T, C); the QKV bias
+        gradient is summed inside the attention backward on the HIP path."""
+        return ops.linear_attention_qkv(x, self.c_attn.weight, self.c_attn.bias, self.n_head)
+
     def forward(self, x, fuse_out_bias=False):
-        # QKV projection + attention; the projection's bias gradient is summed inside the
-        # attention backward on the HIP path
-        y = ops.linear_attention_qkv(x, self.c_attn.weight, self.c_attn.bias, self.n_head)  # (B, T, C)
+        y = self.attend(x)
         # with fuse_out_bias the caller adds c_proj.bias inside its add+LayerNorm kernel
         y = ops.linear(y, self.c_proj.weight, None if fuse_out_bias else self.c_proj.bias)
         if self.dropout and self.training:
@@ -173,13 +176,23 @@ class GPT(nn.Module):
         # The branch output-projection biases are folded into the same kernel
         # (forward: added before the residual sum; backward: their gradient is a
         # column sum of the residual-stream gradient the kernel already holds).
+        # Without dropout the branch output projections do the residual add themselves (one
+        # GEMM with the bias and the old stream in its epilogue; the LayerNorm then reads only
+        # the new stream: ops/residual.py).
+        fused_sites = not (self.config.dropout and self.training)
         for i, block in enumerate(blocks):
-            a = block.attn(h, fuse_out_bias=True)
-            x, h = ops.add_layer_norm(x, a, block.ln_2.weight, block.ln_2.bias,
-                                      r_bias=block.attn.c_proj.bias)
-            m = block.mlp(h, fuse_out_bias=True)
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else self.transformer.ln_f
-            x, h = ops.add_layer_norm(x, m, nxt.weight, nxt.bias, r_bias=block.mlp.c_proj.bias)
+            at, ml = block.attn, block.mlp
+            if fused_sites:
+                x, h = ops.linear_residual_layer_norm(x, at.attend(h), at.c_proj.weight, at.c_proj.bias,
+                                                      block.ln_2.weight, block.ln_2.bias)
+                x, h = ops.mlp_residual_layer_norm(x, h, ml.c_fc.weight, ml.c_fc.bias, ml.c_proj.weight,
+                                                   ml.c_proj.bias, nxt.weight, nxt.bias)
+                continue
+            a = at(h, fuse_out_bias=True)
+            x, h = ops.add_layer_norm(x, a, block.ln_2.weight, block.ln_2.bias, r_bias=at.c_proj.bias)
+            m = ml(h, fuse_out_bias=True)
+            x, h = ops.add_layer_norm(x, m, nxt.weight, nxt.bias, r_bias=ml.c_proj.bias)
         x = h
         if targets is not None:
             loss = ops.linear_cross_entropy(x.reshape(B * T, -1), self.lm_head.weight,

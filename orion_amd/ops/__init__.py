@@ -69,6 +69,28 @@ def add_layer_norm(x, r, weight, bias, eps=1e-5, r_bias=None):
     return s, layer_norm(s, weight, bias, eps)
 
 
+def linear_residual_layer_norm(x, inp, w, rb, ln_w, ln_b, eps=1e-5):
+    """A residual site with the branch's output projection: (s, y) = (x + inp W^T + rb,
+    LayerNorm(s)).  On the GPU one hipBLASLt GEMM with the bias and the old stream in its
+    epilogue, then a LayerNorm that reads only s (ops/residual.py); elsewhere the projection
+    then :func:`add_layer_norm`."""
+    if _gpu(x) == "hip":
+        from .residual import eligible, linear_residual_layer_norm_hip
+        if eligible(x, inp, w, rb):
+            return linear_residual_layer_norm_hip(x, inp, w, rb, ln_w, ln_b, eps)
+    return add_layer_norm(x, linear(inp, w, None), ln_w, ln_b, eps, r_bias=rb)
+
+
+def mlp_residual_layer_norm(x, h, w_fc, b_fc, w_proj, b_proj, ln_w, ln_b, eps=1e-5):
+    """The MLP residual site: (s, y) = (x + mlp(h), LayerNorm(s)) with GPT-2's MLP; on the GPU
+    the fused MLP whose fc2 GEMM does the residual add (ops/residual.py)."""
+    if _gpu(x) == "hip":
+        from .residual import mlp_eligible, mlp_residual_layer_norm_hip
+        if mlp_eligible(x, h, w_fc, w_proj, b_proj):
+            return mlp_residual_layer_norm_hip(x, h, w_fc, b_fc, w_proj, b_proj, ln_w, ln_b, eps)
+    return add_layer_norm(x, mlp(h, w_fc, b_fc, w_proj, None), ln_w, ln_b, eps, r_bias=b_proj)
+
+
 def add_rms_norm(x, r, weight, eps=1e-5):
     """Fused residual add + RMSNorm: (s, y) = (x + r, RMSNorm(x + r))."""
     b = _gpu(x)
@@ -308,7 +330,7 @@ __all__ = [
     "layer_norm", "rms_norm", "gelu", "bias_gelu", "swiglu", "add_broadcast", "embed_layer_norm",
     "token_embedding", "rope",
     "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "linear_rope_attention",
-    "cross_entropy", "swiglu_mlp",
+    "cross_entropy", "swiglu_mlp", "linear_residual_layer_norm", "mlp_residual_layer_norm",
     "linear_cross_entropy",
 ]
 

@@ -155,16 +155,7 @@ class _FusedMLP(torch.autograd.Function):
     def forward(ctx, x, w_fc, b_fc, w_proj, b_proj):
         C_ = x.shape[-1]
         x2 = x.reshape(-1, C_)
-        bb = None if b_fc is None else b_fc.to(torch.bfloat16)
-        ctx.deriv = False
-        if bb is None:
-            a = linear_fwd(x2, w_fc)
-            h = C().bias_gelu_fwd(a, None).view(a.shape)
-        elif _GELU_DERIV:  # a = GELU'(x W_fc^T + b_fc): the backward epilogue only multiplies
-            a, h = C().gemm(x2, w_fc, False, EPI_BIAS_GELU | GEMM_DERIV, bb, None)
-            ctx.deriv = True
-        else:
-            a, h = C().gemm(x2, w_fc, False, EPI_BIAS_GELU, bb, None)
+        a, h, ctx.deriv = mlp_fc_forward(x2, w_fc, b_fc)
         y = linear_fwd(h, w_proj, b_proj)
         ctx.save_for_backward(x2, a, h, w_fc, w_proj)
         ctx.biases = (b_fc, b_proj)
@@ -175,45 +166,71 @@ class _FusedMLP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, a, h, w_fc, w_proj = ctx.saved_tensors
-        b_fc, b_proj = ctx.biases
-        s_fc, s_proj = ctx.sinks
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        sbfc, sbproj = _claim((b_fc, b_proj))
-        # a already holds the fc bias: GELU'(a), no bias operand (or a IS the derivative)
-        da, dbfc = C().gemm_gelu_bwd(dy2, w_proj, a, None, _view(sbfc), ctx.deriv)
-        _notify(sbfc)
-        dbfc = None if b_fc is None else _unless(dbfc, sbfc)
-        grads = [None, None, None, None, None]
-
-        def proj_grads():
-            if ctx.needs_input_grad[3]:
-                if s_proj is not None:
-                    wgrad_into(dy2, h, s_proj.view, s_proj.take())
-                    s_proj.notify()
-                else:
-                    grads[3] = wgrad(dy2, h)
-            if b_proj is not None and ctx.needs_input_grad[4]:
-                db = C().colsum(dy2, _view(sbproj))
-                grads[4] = None if sbproj is not None else db.to(b_proj.dtype)
-                _notify(sbproj)
-
-        def fc_dgrad():
-            if ctx.needs_input_grad[0]:
-                grads[0] = linear_dgrad(da, w_fc).view(ctx.x_shape)
-
-        def fc_wgrad():
-            if ctx.needs_input_grad[1]:
-                if s_fc is not None:
-                    wgrad_into(da, x2, s_fc.view, s_fc.take())
-                    s_fc.notify()
-                else:
-                    grads[1] = wgrad(da, x2)
-        for step in {"0": (proj_grads, fc_dgrad, fc_wgrad), "1": (fc_dgrad, fc_wgrad, proj_grads),
-                     "2": (fc_wgrad, fc_dgrad, proj_grads)}[_MLP_BWD_ORDER]:
-            step()
-        if dbfc is not None:
-            grads[2] = dbfc.to(b_fc.dtype)
+        grads = mlp_backward(dy2, x2, a, h, w_fc, w_proj, ctx.biases, ctx.sinks, ctx.deriv,
+                             ctx.needs_input_grad, proj_bias_grad=True)
+        grads[0] = None if grads[0] is None else grads[0].view(ctx.x_shape)
         return tuple(grads)
+
+
+def mlp_fc_forward(x2, w_fc, b_fc):
+    """(a, h, deriv) of the fused MLP's first GEMM: h = gelu(x W_fc^T + b_fc) and a = the
+    pre-activation, or GELU'(pre-activation) when ``deriv`` (_GELU_DERIV)."""
+    bb = None if b_fc is None else b_fc.to(torch.bfloat16)
+    if bb is None:
+        a = linear_fwd(x2, w_fc)
+        return a, C().bias_gelu_fwd(a, None).view(a.shape), False
+    if _GELU_DERIV:  # a = GELU'(x W_fc^T + b_fc): the backward epilogue only multiplies
+        a, h = C().gemm(x2, w_fc, False, EPI_BIAS_GELU | GEMM_DERIV, bb, None)
+        return a, h, True
+    a, h = C().gemm(x2, w_fc, False, EPI_BIAS_GELU, bb, None)
+    return a, h, False
+
+
+def mlp_backward(dy2, x2, a, h, w_fc, w_proj, biases, sinks, deriv, needs, proj_bias_grad=True):
+    """Gradients [dx2, dW_fc, db_fc, dW_proj, db_proj] of the fused MLP from dy2 = d(output)
+    (rows, C): one in-tree GEMM dy W_proj with GELU' and the fc-bias column sums in its
+    epilogue, then the weight gradients (straight into the arena through ``sinks``) and the fc
+    input gradient in the _MLP_BWD_ORDER order.  ``needs`` = needs_input_grad of (x, w_fc,
+    b_fc, w_proj, b_proj); without ``proj_bias_grad`` the caller owns db_proj."""
+    b_fc, b_proj = biases
+    s_fc, s_proj = sinks
+    sbfc, sbproj = _claim((b_fc, b_proj if proj_bias_grad else None))
+    # a already holds the fc bias: GELU'(a), no bias operand (or a IS the derivative)
+    da, dbfc = C().gemm_gelu_bwd(dy2, w_proj, a, None, _view(sbfc), deriv)
+    _notify(sbfc)
+    dbfc = None if b_fc is None else _unless(dbfc, sbfc)
+    grads = [None, None, None, None, None]
+
+    def proj_grads():
+        if needs[3]:
+            if s_proj is not None:
+                wgrad_into(dy2, h, s_proj.view, s_proj.take())
+                s_proj.notify()
+            else:
+                grads[3] = wgrad(dy2, h)
+        if proj_bias_grad and b_proj is not None and needs[4]:
+            db = C().colsum(dy2, _view(sbproj))
+            grads[4] = None if sbproj is not None else db.to(b_proj.dtype)
+            _notify(sbproj)
+
+    def fc_dgrad():
+        if needs[0]:
+            grads[0] = linear_dgrad(da, w_fc)
+
+    def fc_wgrad():
+        if needs[1]:
+            if s_fc is not None:
+                wgrad_into(da, x2, s_fc.view, s_fc.take())
+                s_fc.notify()
+            else:
+                grads[1] = wgrad(da, x2)
+    for step in {"0": (proj_grads, fc_dgrad, fc_wgrad), "1": (fc_dgrad, fc_wgrad, proj_grads),
+                 "2": (fc_wgrad, fc_dgrad, proj_grads)}[_MLP_BWD_ORDER]:
+        step()
+    if dbfc is not None:
+        grads[2] = dbfc.to(b_fc.dtype)
+    return grads
 
 
 # ORION_GELU_DERIV=1 (default, round 5): the fused MLP's forward epilogue stores GELU'(a) in

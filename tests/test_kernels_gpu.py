@@ -74,6 +74,48 @@ def test_add_layernorm_fwd_bwd():
               (sr, yr, xr.grad, rr.grad, wr.grad, br.grad), (sb, yb, *(t.grad for t in lb)))
 
 
+def _site_ref(x, inp, w, rb, lw, lb, fc=None):
+    """s = x + branch W^T + rb (branch = inp, or gelu(inp W_fc^T + b_fc) for the MLP site),
+    y = LayerNorm(s)."""
+    br = inp if fc is None else F.gelu(inp @ fc[0].t() + fc[1], approximate="tanh")
+    s = x + br @ w.t() + rb
+    return s, F.layer_norm(s, (x.shape[-1],), lw, lb, 1e-5)
+
+
+@pytest.mark.parametrize("site", ["linear", "mlp"])
+def test_residual_sites_fwd_bwd(site):
+    """ops.linear_residual_layer_norm / mlp_residual_layer_norm (the branch output projection
+    doing the residual add in a hipBLASLt epilogue, csrc/blaslt.cpp, then the LayerNorm): the
+    stream and the normalised output and every gradient (stream, branch input, projection,
+    its bias, the fc GEMM for the MLP, the LayerNorm weights) against fp32 autograd and the
+    bf16 torch composition, ragged token count."""
+    from orion_amd.ops import residual as R
+    torch.manual_seed(1)
+    C, F4 = 768, 3072
+    x, inp = bf(3, 333, C), bf(3, 333, C)
+    w, rb = (0.05 * torch.randn(C, F4 if site == "mlp" else C, device=DEV)).bfloat16(), bf(C) * 0.1
+    lw = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16()
+    lb = (0.1 * torch.randn(C, device=DEV)).bfloat16()
+    fc = ((0.05 * torch.randn(F4, C, device=DEV)).bfloat16(), bf(F4) * 0.1) if site == "mlp" else None
+    ts = [t.clone().requires_grad_() for t in (x, inp, w, rb, lw, lb) + (fc or ())]
+    assert R.eligible(ts[0], ts[1], ts[2], ts[3])
+    if site == "mlp":
+        s, y = ops.mlp_residual_layer_norm(ts[0], ts[1], ts[6], ts[7], ts[2], ts[3], ts[4], ts[5])
+    else:
+        s, y = ops.linear_residual_layer_norm(*ts)
+    ds, dy = bf(3, 333, C), bf(3, 333, C)
+    torch.autograd.backward((s, y), (ds, dy))
+    fs = [t.detach().float().requires_grad_() for t in ts]
+    sr, yr = _site_ref(*fs[:6], fc=(fs[6], fs[7]) if site == "mlp" else None)
+    torch.autograd.backward((sr, yr), (ds.float(), dy.float()))
+    bs = [t.detach().clone().requires_grad_() for t in ts]
+    sb, yb = _site_ref(*bs[:6], fc=(bs[6], bs[7]) if site == "mlp" else None)
+    torch.autograd.backward((sb, yb), (ds, dy))
+    names = ["dx", "dinp", "dw", "drb", "dlw", "dlb"] + (["dwfc", "dbfc"] if site == "mlp" else [])
+    check_all(["s", "y"] + names, [s, y] + [t.grad for t in ts], [sr, yr] + [t.grad for t in fs],
+              [sb, yb] + [t.grad for t in bs])
+
+
 @pytest.mark.parametrize("C", [4096, 2048, 768])
 def test_rmsnorm_fwd_bwd(C):
     torch.manual_seed(0)
