@@ -1,6 +1,6 @@
 // hipBLASLt matmul with the residual add and the bias in its epilogue (round 6):
 //
-//   D[M][N] = X[M][K] W[N][K]^T + bias[N] + R[M][N]        (row-major bf16, fp32 accumulate)
+//   D[M][N] = X[M][K] W[N][K]^T (+ bias[N]) + R[M][N]      (row-major bf16, fp32 accumulate)
 //
 // GPT-2's branch output projections (attn c_proj, mlp c_proj) feed the residual stream: with
 // the add here, the LayerNorm that follows reads only the new stream s = D instead of the old
@@ -37,7 +37,7 @@ struct Plan {
   bool tuned = false;
 };
 
-using Key = std::tuple<int, int, int, int, long, long, long, long>;
+using Key = std::tuple<int, int, int, int, long, long, long, long, bool>;
 
 std::mutex g_mu;
 hipblasLtHandle_t g_handle[kMaxDev] = {};
@@ -46,7 +46,7 @@ std::map<Key, Plan> g_plans;
 
 bool ok(hipblasStatus_t s) { return s == HIPBLAS_STATUS_SUCCESS; }
 
-int make_plan(int dev, int M, int N, int K, long ldx, long ldw, long ldr, long ldd, Plan& p) {
+int make_plan(int dev, int M, int N, int K, long ldx, long ldw, long ldr, long ldd, bool has_bias, Plan& p) {
   if (!g_handle[dev]) {
     if (!ok(hipblasLtCreate(&g_handle[dev]))) return -10;
     if (hipMalloc(&g_ws[dev], kWorkspace) != hipSuccess) return -11;
@@ -55,10 +55,12 @@ int make_plan(int dev, int M, int N, int K, long ldx, long ldw, long ldr, long l
   const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-  const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
+  const hipblasLtEpilogue_t epi = has_bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
-  const hipDataType bt = HIP_R_16BF;
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  if (has_bias) {
+    const hipDataType bt = HIP_R_16BF;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  }
   if (!ok(hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16BF, K, N, ldw)) ||
       !ok(hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16BF, K, M, ldx)) ||
       !ok(hipblasLtMatrixLayoutCreate(&p.c, HIP_R_16BF, N, M, ldr)) ||
@@ -97,21 +99,22 @@ int make_plan(int dev, int M, int N, int K, long ldx, long ldw, long ldr, long l
 
 int orion_blaslt_linear_res(const void* X, long ldx, const void* W, long ldw, const void* bias, const void* R,
                             long ldr, void* D, long ldd, int M, int N, int K, hipStream_t st) {
-  if (M < 1 || N < 1 || K < 1 || !bias) return -1;
+  if (M < 1 || N < 1 || K < 1) return -1;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return -2;
   std::lock_guard<std::mutex> lock(g_mu);
-  const Key key{dev, M, N, K, ldx, ldw, ldr, ldd};
+  const bool has_bias = bias != nullptr;
+  const Key key{dev, M, N, K, ldx, ldw, ldr, ldd, has_bias};
   auto it = g_plans.find(key);
   if (it == g_plans.end()) {
     Plan p;
-    const int rc = make_plan(dev, M, N, K, ldx, ldw, ldr, ldd, p);
+    const int rc = make_plan(dev, M, N, K, ldx, ldw, ldr, ldd, has_bias, p);
     if (rc) return rc;
     it = g_plans.emplace(key, p).first;
   }
   Plan& p = it->second;
   // the bias pointer is per call (the desc is shared by every call of this shape)
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+  if (has_bias) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
   const float alpha = 1.f, beta = 1.f;
   auto run = [&](const hipblasLtMatmulAlgo_t& algo) {
     return hipblasLtMatmul(g_handle[dev], p.desc, &alpha, W, p.a, X, p.b, &beta, R, p.c, D, p.d, &algo,

@@ -75,11 +75,15 @@ class Attention(nn.Module):
         self.qkv_proj = nn.Linear(cfg.dim, (cfg.n_heads + 2 * cfg.n_kv_heads) * cfg.head_dim, bias=False)
         self.o_proj = nn.Linear(cfg.n_heads * cfg.head_dim, cfg.dim, bias=False)
 
-    def forward(self, x, cos, sin, pos0=0):
+    def attend(self, x, cos, sin, pos0=0):
+        """QKV projection + RoPE + attention, before o_proj: (B, T, Hq * D).  On the GPU with
+        D = 128 the rotation rides in the projection's epilogue."""
         B, T, _ = x.shape
-        # (B, T, Hq, D); on the GPU with D = 128 the rotation rides in the projection's epilogue
         o = ops.linear_rope_attention(x, self.qkv_proj.weight, self.n_heads, self.n_kv, cos, sin, pos0)
-        return ops.linear(o.reshape(B, T, -1), self.o_proj.weight)
+        return o.reshape(B, T, -1)
+
+    def forward(self, x, cos, sin, pos0=0):
+        return ops.linear(self.attend(x, cos, sin, pos0), self.o_proj.weight)
 
 
 class FeedForward(nn.Module):
@@ -147,13 +151,15 @@ class Llama(nn.Module):
         cos, sin = self.rope_cos, self.rope_sin
         layers = self.layers
         h = layers[0].input_layernorm(x)
+        # the o_proj / down_proj GEMMs add the residual stream in their epilogue and the
+        # RMSNorm reads only the new stream (ops/residual.py; other backends: add_rms_norm)
         for i, layer in enumerate(layers):
-            a = layer.self_attn(h, cos, sin, pos0)
-            x, h = ops.add_rms_norm(x, a, layer.post_attention_layernorm.weight,
-                                    layer.post_attention_layernorm.eps)
-            m = layer.mlp(h)
+            at, ff, pln = layer.self_attn, layer.mlp, layer.post_attention_layernorm
+            x, h = ops.linear_residual_rms_norm(x, at.attend(h, cos, sin, pos0), at.o_proj.weight,
+                                                pln.weight, pln.eps)
             nxt = layers[i + 1].input_layernorm if i + 1 < len(layers) else self.norm
-            x, h = ops.add_rms_norm(x, m, nxt.weight, nxt.eps)
+            x, h = ops.swiglu_residual_rms_norm(x, h, ff.gate_up_proj.weight, ff.down_proj.weight,
+                                                nxt.weight, nxt.eps)
         if targets is not None:
             loss = ops.linear_cross_entropy(h.reshape(B * T, -1), self.lm_head.weight,
                                             targets.reshape(-1), ignore_index=-1)

@@ -91,6 +91,26 @@ def mlp_residual_layer_norm(x, h, w_fc, b_fc, w_proj, b_proj, ln_w, ln_b, eps=1e
     return add_layer_norm(x, mlp(h, w_fc, b_fc, w_proj, None), ln_w, ln_b, eps, r_bias=b_proj)
 
 
+def linear_residual_rms_norm(x, inp, w, nw, eps=1e-5):
+    """Llama's attention site: (s, y) = (x + inp W^T, RMSNorm(s)); on the GPU the o_proj GEMM adds
+    the residual stream in its epilogue and the RMSNorm reads only s (ops/residual.py)."""
+    if _gpu(x) == "hip":
+        from .residual import eligible, linear_residual_rms_norm_hip
+        if eligible(x, inp, w, None, need_bias=False):
+            return linear_residual_rms_norm_hip(x, inp, w, nw, eps)
+    return add_rms_norm(x, linear(inp, w), nw, eps)
+
+
+def swiglu_residual_rms_norm(x, h, w_gate_up, w_down, nw, eps=1e-5):
+    """Llama's feed-forward site: (s, y) = (x + swiglu_mlp(h), RMSNorm(s)); on the GPU down_proj
+    adds the residual stream in its epilogue (ops/residual.py)."""
+    if _gpu(x) == "hip":
+        from .residual import swiglu_eligible, swiglu_residual_rms_norm_hip
+        if swiglu_eligible(x, h, w_gate_up, w_down):
+            return swiglu_residual_rms_norm_hip(x, h, w_gate_up, w_down, nw, eps)
+    return add_rms_norm(x, swiglu_mlp(h, w_gate_up, w_down), nw, eps)
+
+
 def add_rms_norm(x, r, weight, eps=1e-5):
     """Fused residual add + RMSNorm: (s, y) = (x + r, RMSNorm(x + r))."""
     b = _gpu(x)
@@ -331,6 +351,7 @@ __all__ = [
     "token_embedding", "rope",
     "attention_qkv", "linear_attention_qkv", "attention", "rope_attention_packed", "linear_rope_attention",
     "cross_entropy", "swiglu_mlp", "linear_residual_layer_norm", "mlp_residual_layer_norm",
+    "linear_residual_rms_norm", "swiglu_residual_rms_norm",
     "linear_cross_entropy",
 ]
 

@@ -298,11 +298,7 @@ class _SwigluMLP(torch.autograd.Function):
     def forward(ctx, x, w_gu, w_down):
         C_ = x.shape[-1]
         x2 = x.reshape(-1, C_)
-        if _SWIGLU_FWD == "gemm" and w_gu.shape[0] % 256 == 0 and w_gu.numel() * 2 < 0xFFFFFF00:
-            gu, h = C().gemm_swiglu(x2, w_gu)
-        else:
-            gu = linear_fwd(x2, w_gu)
-            h = C().swiglu_fwd(gu)
+        gu, h = swiglu_forward(x2, w_gu)
         y = linear_fwd(h, w_down)
         ctx.save_for_backward(x2, gu, h, w_gu, w_down)
         ctx.sinks = (sink_of(w_gu), sink_of(w_down))
@@ -312,35 +308,52 @@ class _SwigluMLP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, gu, h, w_gu, w_down = ctx.saved_tensors
-        s_gu, s_down = ctx.sinks
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        dgu = C().gemm_swiglu_bwd(dy2, w_down, gu)
-        grads = [None, None, None]
-
-        def down_wgrad():
-            if ctx.needs_input_grad[2]:
-                if s_down is not None:
-                    wgrad_into(dy2, h, s_down.view, s_down.take())
-                    s_down.notify()
-                else:
-                    grads[2] = wgrad(dy2, h)
-
-        def gu_dgrad():
-            if ctx.needs_input_grad[0]:
-                grads[0] = linear_dgrad(dgu, w_gu).view(ctx.x_shape)
-
-        def gu_wgrad():
-            if ctx.needs_input_grad[1]:
-                if s_gu is not None:
-                    wgrad_into(dgu, x2, s_gu.view, s_gu.take())
-                    s_gu.notify()
-                else:
-                    grads[1] = wgrad(dgu, x2)
-        # the same orders as _FusedMLP (_SWIGLU_BWD_ORDER)
-        for step in {"0": (down_wgrad, gu_dgrad, gu_wgrad), "1": (gu_dgrad, gu_wgrad, down_wgrad),
-                     "2": (gu_wgrad, gu_dgrad, down_wgrad)}[_SWIGLU_BWD_ORDER]:
-            step()
+        grads = swiglu_backward(dy2, x2, gu, h, w_gu, w_down, ctx.sinks, ctx.needs_input_grad)
+        grads[0] = None if grads[0] is None else grads[0].view(ctx.x_shape)
         return tuple(grads)
+
+
+def swiglu_forward(x2, w_gu):
+    """(gu, h) of Llama's feed-forward input side: gu = x W_gu^T, h = silu(gate) * up."""
+    if _SWIGLU_FWD == "gemm" and w_gu.shape[0] % 256 == 0 and w_gu.numel() * 2 < 0xFFFFFF00:
+        return tuple(C().gemm_swiglu(x2, w_gu))
+    gu = linear_fwd(x2, w_gu)
+    return gu, C().swiglu_fwd(gu)
+
+
+def swiglu_backward(dy2, x2, gu, h, w_gu, w_down, sinks, needs):
+    """Gradients [dx2, dW_gu, dW_down] of the feed-forward from dy2 = d(output): ONE in-tree GEMM
+    dy W_down whose epilogue applies SwiGLU' (EPI_SWIGLU_BWD), then the weight gradients
+    (through ``sinks``) and the input gradient in the _SWIGLU_BWD_ORDER order."""
+    s_gu, s_down = sinks
+    dgu = C().gemm_swiglu_bwd(dy2, w_down, gu)
+    grads = [None, None, None]
+
+    def down_wgrad():
+        if needs[2]:
+            if s_down is not None:
+                wgrad_into(dy2, h, s_down.view, s_down.take())
+                s_down.notify()
+            else:
+                grads[2] = wgrad(dy2, h)
+
+    def gu_dgrad():
+        if needs[0]:
+            grads[0] = linear_dgrad(dgu, w_gu)
+
+    def gu_wgrad():
+        if needs[1]:
+            if s_gu is not None:
+                wgrad_into(dgu, x2, s_gu.view, s_gu.take())
+                s_gu.notify()
+            else:
+                grads[1] = wgrad(dgu, x2)
+    # the same orders as _FusedMLP (_SWIGLU_BWD_ORDER)
+    for step in {"0": (down_wgrad, gu_dgrad, gu_wgrad), "1": (gu_dgrad, gu_wgrad, down_wgrad),
+                 "2": (gu_wgrad, gu_dgrad, down_wgrad)}[_SWIGLU_BWD_ORDER]:
+        step()
+    return grads
 
 
 def swiglu_mlp_hip(x, w_gu, w_down):

@@ -28,7 +28,8 @@ import os
 import torch
 
 from ._ext import C
-from .activations import mlp_backward, mlp_fc_forward, mlp_ok
+from .activations import (mlp_backward, mlp_fc_forward, mlp_ok, swiglu_backward, swiglu_forward,
+                          swiglu_mlp_ok)
 from .determinism import deterministic
 from .grad_sink import sink_of
 from .layernorm import _bf16, _claim, _grad, _notify, _unless, _view, linear_input_weight_grads
@@ -40,10 +41,13 @@ _RESID_GEMM = _MODE != "0"
 _RESID_MLP = _MODE not in ("0", "attn")
 
 
-def eligible(x, inp, w, rb) -> bool:
-    return (_RESID_GEMM and rb is not None and not deterministic() and x.is_cuda
-            and x.dtype == inp.dtype == w.dtype == rb.dtype == torch.bfloat16
-            and x.is_contiguous() and inp.is_contiguous() and w.is_contiguous() and rb.is_contiguous())
+def eligible(x, inp, w, rb, need_bias=True) -> bool:
+    if rb is None and need_bias:
+        return False
+    return (_RESID_GEMM and not deterministic() and x.is_cuda
+            and x.dtype == inp.dtype == w.dtype == torch.bfloat16 and x.is_contiguous()
+            and inp.is_contiguous() and w.is_contiguous()
+            and (rb is None or (rb.dtype == torch.bfloat16 and rb.is_contiguous())))
 
 
 _CHECKED = set()
@@ -54,9 +58,11 @@ def _residual_gemm(inp2, w, rb, x2):
     solution by timing) is checked against the torch composition, so a solution that accepted
     the problem but computed something else fails loudly instead of training on it."""
     s2 = C().linear_residual(inp2, w, rb, x2)
-    key = (inp2.device, tuple(inp2.shape), tuple(w.shape))
+    key = (inp2.device, tuple(inp2.shape), tuple(w.shape), rb is None)
     if key not in _CHECKED:
-        ref = torch.addmm(rb.float(), inp2.float(), w.float().t()) + x2.float()
+        ref = inp2.float() @ w.float().t() + x2.float()
+        if rb is not None:
+            ref += rb.float()
         err = ((s2.float() - ref).norm() / ref.norm().clamp_min(1e-30)).item()
         if not err < 1e-2:
             raise RuntimeError(f"linear_residual {tuple(inp2.shape)} x {tuple(w.shape)}: relative error {err:.3g}")
@@ -158,3 +164,87 @@ def mlp_residual_layer_norm_hip(x, h, w_fc, b_fc, w_proj, b_proj, ln_w, ln_b, ep
 
 def mlp_eligible(x, h, w_fc, w_proj, b_proj) -> bool:
     return _RESID_MLP and eligible(x, h, w_proj, b_proj) and mlp_ok(h, w_fc, w_proj)
+
+
+# ---------------------------------------------------------------- Llama: RMSNorm sites (no biases)
+def _rms_forward(ctx, s2, w, eps):
+    y, rstd = C().rmsnorm_fwd(s2, _bf16(w), float(eps))
+    ctx.rstd = rstd
+    return y
+
+
+def _rms_backward(ctx, s2, w, ds, dy):
+    if dy is None:
+        dy = torch.zeros_like(s2)
+    dres = None if ds is None else ds.reshape(s2.shape).contiguous()
+    (sw,) = _claim((w,))
+    dsum, dw = C().rmsnorm_bwd(dy.reshape(s2.shape).contiguous(), s2, _bf16(w), ctx.rstd, dres, _view(sw))
+    _notify(sw)
+    return dsum, _grad(_unless(dw, sw), w.dtype)
+
+
+class _LinearResidualRMS(torch.autograd.Function):
+    """(s, y) = (x + inp W^T, RMSNorm(s)): Llama's attention site (o_proj)."""
+
+    @staticmethod
+    def forward(ctx, x, inp, w, nw, eps):
+        C_ = x.shape[-1]
+        inp2 = inp.reshape(-1, inp.shape[-1])
+        s2 = _residual_gemm(inp2, w, None, x.reshape(-1, C_))
+        y = _rms_forward(ctx, s2, nw, eps)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(s2, inp2, w, nw)
+        ctx.sink = sink_of(w)
+        ctx.inp_shape = inp.shape
+        return s2.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s2, inp2, w, nw = ctx.saved_tensors
+        dsum, dnw = _rms_backward(ctx, s2, nw, ds, dy)
+        dinp, dw = linear_input_weight_grads(dsum, inp2, w, ctx.sink, ctx.needs_input_grad[1],
+                                             ctx.needs_input_grad[2])
+        dx = dsum.view(ctx.inp_shape[:-1] + (s2.shape[-1],)) if ctx.needs_input_grad[0] else None
+        dinp = None if dinp is None else dinp.view(ctx.inp_shape)
+        return dx, dinp, dw, dnw, None
+
+
+class _SwigluResidualRMS(torch.autograd.Function):
+    """(s, y) = (x + swiglu(h W_gu^T) W_down^T, RMSNorm(s)): Llama's feed-forward site (the
+    SwiGLU forward in the gate_up epilogue, SwiGLU' in the down_proj input-gradient epilogue:
+    ops/activations.py; down_proj is the residual GEMM)."""
+
+    @staticmethod
+    def forward(ctx, x, h, w_gu, w_down, nw, eps):
+        C_ = x.shape[-1]
+        h2 = h.reshape(-1, C_)
+        gu, g = swiglu_forward(h2, w_gu)
+        s2 = _residual_gemm(g, w_down, None, x.reshape(-1, C_))
+        y = _rms_forward(ctx, s2, nw, eps)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(s2, h2, gu, g, w_gu, w_down, nw)
+        ctx.sinks = (sink_of(w_gu), sink_of(w_down))
+        ctx.x_shape = x.shape
+        return s2.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s2, h2, gu, g, w_gu, w_down, nw = ctx.saved_tensors
+        dsum, dnw = _rms_backward(ctx, s2, nw, ds, dy)
+        n = ctx.needs_input_grad
+        dh, dwgu, dwd = swiglu_backward(dsum, h2, gu, g, w_gu, w_down, ctx.sinks, (n[1], n[2], n[3]))
+        dx = dsum.view(ctx.x_shape) if n[0] else None
+        dh = None if dh is None else dh.view(ctx.x_shape)
+        return dx, dh, dwgu, dwd, dnw, None
+
+
+def linear_residual_rms_norm_hip(x, inp, w, nw, eps=1e-5):
+    return _LinearResidualRMS.apply(x, inp, w, nw, eps)
+
+
+def swiglu_residual_rms_norm_hip(x, h, w_gu, w_down, nw, eps=1e-5):
+    return _SwigluResidualRMS.apply(x, h, w_gu, w_down, nw, eps)
+
+
+def swiglu_eligible(x, h, w_gu, w_down) -> bool:
+    return _RESID_MLP and eligible(x, h, w_down, None, need_bias=False) and swiglu_mlp_ok(h, w_gu, w_down)

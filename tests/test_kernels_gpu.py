@@ -116,6 +116,46 @@ def test_residual_sites_fwd_bwd(site):
               [sb, yb] + [t.grad for t in bs])
 
 
+def _rms_site_ref(x, inp, w, nw, gu=None):
+    br = inp
+    if gu is not None:
+        g, u = (inp @ gu.t()).chunk(2, -1)
+        br = F.silu(g) * u
+    s = x + br @ w.t()
+    sf = s.float()
+    return s, (sf * torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + 1e-5)).to(s.dtype) * nw
+
+
+@pytest.mark.parametrize("site", ["linear", "swiglu"])
+def test_llama_residual_sites_fwd_bwd(site):
+    """ops.linear_residual_rms_norm / swiglu_residual_rms_norm (Llama: o_proj / down_proj add
+    the residual stream in the hipBLASLt epilogue, then RMSNorm reads only the new stream):
+    stream, normalised output and every gradient against fp32 autograd and the bf16 torch
+    composition, ragged token count."""
+    torch.manual_seed(2)
+    C, F_ = 512, 1408
+    x, inp = bf(2, 177, C), bf(2, 177, C)
+    w = (0.05 * torch.randn(C, F_ if site == "swiglu" else C, device=DEV)).bfloat16()
+    nw = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16()
+    gu = (0.05 * torch.randn(2 * F_, C, device=DEV)).bfloat16() if site == "swiglu" else None
+    ts = [t.clone().requires_grad_() for t in (x, inp, w, nw) + ((gu,) if gu is not None else ())]
+    if site == "swiglu":
+        s, y = ops.swiglu_residual_rms_norm(ts[0], ts[1], ts[4], ts[2], ts[3])
+    else:
+        s, y = ops.linear_residual_rms_norm(*ts)
+    ds, dy = bf(2, 177, C), bf(2, 177, C)
+    torch.autograd.backward((s, y), (ds, dy))
+    fs = [t.detach().float().requires_grad_() for t in ts]
+    sr, yr = _rms_site_ref(*fs[:4], gu=fs[4] if site == "swiglu" else None)
+    torch.autograd.backward((sr, yr), (ds.float(), dy.float()))
+    bs = [t.detach().clone().requires_grad_() for t in ts]
+    sb, yb = _rms_site_ref(*bs[:4], gu=bs[4] if site == "swiglu" else None)
+    torch.autograd.backward((sb, yb), (ds, dy))
+    names = ["dx", "dinp", "dw", "dnw"] + (["dwgu"] if site == "swiglu" else [])
+    check_all(["s", "y"] + names, [s, y] + [t.grad for t in ts], [sr, yr] + [t.grad for t in fs],
+              [sb, yb] + [t.grad for t in bs])
+
+
 @pytest.mark.parametrize("C", [4096, 2048, 768])
 def test_rmsnorm_fwd_bwd(C):
     torch.manual_seed(0)
