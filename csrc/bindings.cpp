@@ -502,24 +502,26 @@ Tensor gemm_rope(const Tensor& x, const Tensor& w, const Tensor& cos, const Tens
   return out;
 }
 
-// s (M, N) = x w^T (+ bias) + r: a branch's output projection with the residual add (hipBLASLt, the
+// s (M, N) = x w^T (+ bias) (+ r): a branch's output projection with the residual add (hipBLASLt, the
 // bias and r in its epilogue; csrc/blaslt.cpp).  x (M, K) and r (M, N) with unit column stride.
-Tensor linear_residual(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias_in, const Tensor& r) {
+Tensor linear_residual(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias_in,
+                       const c10::optional<Tensor>& r_in) {
   check_bf16(x, "x");
   check_bf16(w, "w");
-  check_bf16(r, "r");
-  const bool hb = bias_in.has_value() && bias_in->defined();
+  const bool hb = bias_in.has_value() && bias_in->defined(), hr = r_in.has_value() && r_in->defined();
   if (hb) check_bf16(*bias_in, "bias");
-  TORCH_CHECK(x.dim() == 2 && r.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && r.stride(1) == 1 &&
-                  w.is_contiguous() && x.size(1) == w.size(1) && r.size(0) == x.size(0) && r.size(1) == w.size(0) &&
-                  (!hb || (bias_in->is_contiguous() && bias_in->numel() == w.size(0))),
-              "linear_residual: x (M, K), w (N, K), bias (N) or None, r (M, N)");
+  if (hr) check_bf16(*r_in, "r");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.is_contiguous() && x.size(1) == w.size(1) &&
+                  (!hb || (bias_in->is_contiguous() && bias_in->numel() == w.size(0))) &&
+                  (!hr || (r_in->dim() == 2 && r_in->stride(1) == 1 && r_in->size(0) == x.size(0) &&
+                           r_in->size(1) == w.size(0))),
+              "linear_residual: x (M, K), w (N, K), bias (N) or None, r (M, N) or None");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   auto out = at::empty({M, N}, x.options());
   check_launch(orion_blaslt_linear_res(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
-                                       hb ? bias_in->data_ptr() : nullptr,
-                                       r.data_ptr(), r.stride(0), out.data_ptr(), N, (int)M, (int)N, (int)K,
+                                       hb ? bias_in->data_ptr() : nullptr, hr ? r_in->data_ptr() : nullptr,
+                                       hr ? r_in->stride(0) : N, out.data_ptr(), N, (int)M, (int)N, (int)K,
                                        cur_stream()),
                "linear_residual");
   return out;
@@ -1117,7 +1119,7 @@ TORCH_LIBRARY(orion_amd, m) {
   m.def("gemm_rowscale(Tensor e, Tensor w, Tensor srow) -> Tensor");
   m.def("gemm_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int pos0, int T, int rope_cols, int D) -> Tensor");
   m.def("gemm_swiglu(Tensor x, Tensor w) -> Tensor[]");
-  m.def("linear_residual(Tensor x, Tensor w, Tensor? bias, Tensor r) -> Tensor");
+  m.def("linear_residual(Tensor x, Tensor w, Tensor? bias, Tensor? r) -> Tensor");
   m.def("gemm(Tensor x, Tensor w, bool w_kmajor, int epi, Tensor? bias=None, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("gemm_gelu_bwd(Tensor dy, Tensor w, Tensor pre, Tensor? bias=None, Tensor(a!)? db_out=None, bool pre_is_deriv=False) -> (Tensor, Tensor)");
   m.def("gemm_swiglu_bwd(Tensor dy, Tensor w, Tensor gate_up) -> Tensor");

@@ -1,6 +1,6 @@
 // hipBLASLt matmul with the residual add and the bias in its epilogue (round 6):
 //
-//   D[M][N] = X[M][K] W[N][K]^T (+ bias[N]) + R[M][N]      (row-major bf16, fp32 accumulate)
+//   D[M][N] = X[M][K] W[N][K]^T (+ bias[N]) (+ R[M][N])    (row-major bf16, fp32 accumulate)
 //
 // GPT-2's branch output projections (attn c_proj, mlp c_proj) feed the residual stream: with
 // the add here, the LayerNorm that follows reads only the new stream s = D instead of the old
@@ -37,7 +37,7 @@ struct Plan {
   bool tuned = false;
 };
 
-using Key = std::tuple<int, int, int, int, long, long, long, long, bool>;
+using Key = std::tuple<int, int, int, int, long, long, long, long, bool, bool>;
 
 std::mutex g_mu;
 hipblasLtHandle_t g_handle[kMaxDev] = {};
@@ -103,8 +103,9 @@ int orion_blaslt_linear_res(const void* X, long ldx, const void* W, long ldw, co
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return -2;
   std::lock_guard<std::mutex> lock(g_mu);
-  const bool has_bias = bias != nullptr;
-  const Key key{dev, M, N, K, ldx, ldw, ldr, ldd, has_bias};
+  const bool has_bias = bias != nullptr, has_r = R != nullptr;
+  if (!has_r) ldr = ldd;  // beta = 0: C is D's layout (not read)
+  const Key key{dev, M, N, K, ldx, ldw, ldr, ldd, has_bias, has_r};
   auto it = g_plans.find(key);
   if (it == g_plans.end()) {
     Plan p;
@@ -115,9 +116,10 @@ int orion_blaslt_linear_res(const void* X, long ldx, const void* W, long ldw, co
   Plan& p = it->second;
   // the bias pointer is per call (the desc is shared by every call of this shape)
   if (has_bias) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
-  const float alpha = 1.f, beta = 1.f;
+  const float alpha = 1.f, beta = has_r ? 1.f : 0.f;
+  const void* Cp = has_r ? R : D;
   auto run = [&](const hipblasLtMatmulAlgo_t& algo) {
-    return hipblasLtMatmul(g_handle[dev], p.desc, &alpha, W, p.a, X, p.b, &beta, R, p.c, D, p.d, &algo,
+    return hipblasLtMatmul(g_handle[dev], p.desc, &alpha, W, p.a, X, p.b, &beta, Cp, p.c, D, p.d, &algo,
                            g_ws[dev], kWorkspace, st);
   };
   if (!p.tuned) {

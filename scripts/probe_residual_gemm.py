@@ -56,3 +56,13 @@ for name, K in (("attn_proj", 768), ("fc2", 3072)):
                       "add_layernorm_ms": round(t_addln, 4), "layernorm_ms": round(t_ln, 4),
                       "today_ms": round(t_mm + t_addln, 4), "probe_ms": round(t_addmm + t_ln, 4),
                       "blaslt_ms": round(t_res + t_ln, 4)}))
+# plain forwards (no residual): TunableOp-tuned F.linear vs the wrapper's own all-solution search
+for name, N, K in (("qkv+bias", 2304, 768), ("attn_proj", 768, 768), ("fc2", 768, 3072)):
+    h, w, b = mk(M, K), mk(N, K), mk(N)
+    t_lin = med(lambda: torch.nn.functional.linear(h, w, b))
+    t_own = med(lambda: C().linear_residual(h, w, b, None))
+    err = ((C().linear_residual(h, w, b, None).float() - torch.nn.functional.linear(h, w, b).float()).norm()
+           / torch.nn.functional.linear(h, w, b).float().norm()).item()
+    print(json.dumps({"plain": name, "linear_bias_ms": round(t_lin, 4), "wrapper_ms": round(t_own, 4),
+                      "rel_diff": f"{err:.2e}"}))
+
