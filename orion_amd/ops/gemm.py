@@ -164,11 +164,21 @@ def use_hip_gemm(x: torch.Tensor, w: torch.Tensor, w_kmajor: bool) -> bool:
     return _hip_eligible(x, w, w_kmajor)
 
 
+# ORION_FWD_BLASLT=1: plain forwards through the in-tree hipBLASLt wrapper (csrc/blaslt.cpp,
+# every solution timed once per shape) instead of torch's hipBLASLt call (TunableOp's tuned
+# pick where a table entry exists, the library heuristic otherwise); A/B knob
+_FWD_BLASLT = os.environ.get("ORION_FWD_BLASLT", "0") == "1"
+
+
 def linear_fwd(x, w, b=None):
     """x W^T (+ b): csrc/gemm16.hip when selected (see above), else hipBLASLt."""
     if use_hip_gemm(x, w, False):
         return C().gemm(x, w, False, EPI_BIAS if b is not None else EPI_STORE, b, None)[0]
     _note_fallback("linear_fwd", x, w)
+    if (_FWD_BLASLT and x.is_contiguous() and x.dtype == w.dtype == torch.bfloat16
+            and w.is_contiguous() and not deterministic()):
+        y = C().linear_residual(x.reshape(-1, x.shape[-1]), w, b, None)
+        return y.view(*x.shape[:-1], w.shape[0])
     return torch.nn.functional.linear(x, w, b)
 
 
