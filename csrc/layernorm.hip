@@ -10,6 +10,8 @@
 //     registers (the row is read from HBM once);
 //   * backward: a fixed grid of row-chunk workgroups writes fp32 partial column
 //     sums, a second tiny kernel folds them (deterministic, no float atomics).
+#include <cstdlib>
+
 #include "common.h"
 
 // LN_NT: the residual stream sum (saved for the backward, read again by the next block's norm
@@ -158,6 +160,90 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
+  }
+}
+
+// Single-input forward (round 6: the residual sites' LayerNorm reads only the new stream, the
+// branch GEMM having done the add).  gamma / beta stay in registers for the wave's whole row
+// list (the per-row kernel above reloads them, and stand-ins for the absent operands, for every
+// row), and the next row's loads are issued before this row's stores (two register sets), so a
+// wave keeps two rows in flight.
+template <int VEC, int ITERS>
+__global__ __launch_bounds__(256) void ln_fwd1_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int rows, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  typedef typename VecT<VEC>::type VT;
+  float wf[ITERS][VEC], bf[ITERS][VEC];
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int cl = min((i * 64 + lane) * VEC, C - VEC);
+    load_vec<VEC>(w + cl, wf[i]);
+    if (b) load_vec<VEC>(b + cl, bf[i]);
+    else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) bf[i][j] = 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  auto load = [&](int r, VT (&v)[ITERS]) {
+    if (r >= rows) return;  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int cl = min((i * 64 + lane) * VEC, C - VEC);
+      v[i] = *reinterpret_cast<const VT*>(x + (size_t)r * C + cl);
+    }
+  };
+  auto proc = [&](int r, const VT (&v)[ITERS]) {
+    float f[ITERS][VEC];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const bool ok = (i * 64 + lane) * VEC < C;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        f[i][j] = ok ? bf2f(v[i][j]) : 0.f;
+        s += f[i][j];
+      }
+    }
+    const float mean = wave_sum(s) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const bool ok = (i * 64 + lane) * VEC < C;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float d = ok ? f[i][j] - mean : 0.f;
+        q += d * d;
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) * invC + eps);
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int c = (i * 64 + lane) * VEC;
+      if (c < C) {
+        float o[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o[j] = (f[i][j] - mean) * rstd * wf[i][j] + bf[i][j];
+        store_vec<VEC>(y + (size_t)r * C + c, o);
+      }
+    }
+    if (lane == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
+  };
+  VT va[ITERS], vb[ITERS];
+  int r = wid;
+  load(r, va);
+  for (; r < rows; r += 2 * nw) {
+    load(r + nw, vb);
+    proc(r, va);
+    if (r + nw >= rows) break;
+    load(r + 2 * nw, va);
+    proc(r + nw, vb);
   }
 }
 
@@ -469,12 +555,39 @@ static bool ln_pick(int C, int* vec, int* iters, bool exact_fit = false) {
 
 int orion_ln_max_cols() { return 2048; }
 
+// ORION_LN_FWD1=0: the single-input forward through the per-row kernel (A/B);
+// ORION_LN_FWD1_BLOCKS: its workgroup count (default 4096: 4 rows per wave at 65,536 rows;
+// 65,536 x 768: 256 / 512 / 1,024 / 2,048 / 4,096 blocks 67.0 / 41.6 / 36.4 / 36.7 / 35.8 us against
+// 38.9 us for the per-row kernel)
+static int ln_fwd1_blocks() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("ORION_LN_FWD1");
+    const char* nb = getenv("ORION_LN_FWD1_BLOCKS");
+    v = (e && e[0] == '0') ? 0 : (nb ? atoi(nb) : 4096);
+  }
+  return v;
+}
+
 int orion_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
                         float* rstd, int rows, int C, float eps, const void* res, void* sum_out,
                         const void* rbias, hipStream_t st, const int64_t* idx, int T, long V,
                         int* err) {
   int vec, it;
   if (!ln_pick(C, &vec, &it)) return -1;
+  const int nb1 = ln_fwd1_blocks();
+  if (!res && !idx && !rbias && !sum_out && nb1 > 0) {
+    const int blocks = min(nb1, (rows + 3) / 4);
+    auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto B = (const bf16_t*)b; auto Y = (bf16_t*)y;
+#define LNF1(VV, II) ln_fwd1_kernel<VV, II><<<blocks, 256, 0, st>>>(X, W, B, Y, mean, rstd, rows, C, eps)
+    if (vec == 8) {
+      switch (it) { case 1: LNF1(8, 1); break; case 2: LNF1(8, 2); break; case 3: LNF1(8, 3); break; default: LNF1(8, 4); }
+    } else {
+      switch (it) { case 1: LNF1(4, 1); break; case 2: LNF1(4, 2); break; case 3: LNF1(4, 3); break; default: LNF1(4, 4); }
+    }
+#undef LNF1
+    return (int)hipGetLastError();
+  }
   dim3 grid((rows + 3) / 4), block(256);
   auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto B = (const bf16_t*)b;
   auto Y = (bf16_t*)y;
