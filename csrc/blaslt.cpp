@@ -26,7 +26,8 @@
 namespace {
 
 constexpr size_t kWorkspace = 64u << 20;
-constexpr int kCands = 128;  // heuristic candidates timed on first use
+constexpr int kCands = 128;     // heuristic candidates timed on first use
+constexpr int kMaxTimed = 384;  // + supported library solutions, up to this many in total
 constexpr int kMaxDev = 16;
 
 struct Plan {
@@ -85,6 +86,7 @@ int make_plan(int dev, int M, int N, int K, long ldx, long ldw, long ldr, long l
                                     HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F, all))) {
     const float one = 1.f;
     for (auto& r : all) {
+      if ((int)res.size() >= kMaxTimed) break;  // bounds the first call's timing sweep
       size_t need = 0;
       if (ok(hipblaslt_ext::matmulIsAlgoSupported(g_handle[dev], p.desc, &one, p.a, p.b, &one, p.c, p.d, r.algo,
                                                   need)) && need <= kWorkspace)
