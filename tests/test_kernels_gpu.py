@@ -74,6 +74,28 @@ def test_add_layernorm_fwd_bwd():
               (sr, yr, xr.grad, rr.grad, wr.grad, br.grad), (sb, yb, *(t.grad for t in lb)))
 
 
+@pytest.mark.parametrize("bias,resid", [(True, True), (False, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(333, 768, 768), (4096, 768, 3072), (1000, 1152, 256)])
+def test_linear_residual_wrapper(M, N, K, bias, resid):
+    """C().linear_residual (csrc/blaslt.cpp: hipBLASLt with the bias and the residual in its
+    epilogue, the solution chosen by timing on first use) against fp32, with / without either
+    operand, ragged M."""
+    from orion_amd.ops._ext import C
+    torch.manual_seed(M + N + K)
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    b = bf(N, scale=0.1) if bias else None
+    r = bf(M, N) if resid else None
+    got = C().linear_residual(x, w, b, r)
+    want = x.float() @ w.float().t()
+    base = (x @ w.t()).float()
+    if bias:
+        want, base = want + b.float(), base + b.float()
+    if resid:
+        want, base = want + r.float(), base + r.float()
+    assert got.shape == (M, N) and got.dtype == torch.bfloat16
+    within_bf16_budget("linear_residual", got, want, base.bfloat16())
+
+
 def _site_ref(x, inp, w, rb, lw, lb, fc=None):
     """s = x + branch W^T + rb (branch = inp, or gelu(inp W_fc^T + b_fc) for the MLP site),
     y = LayerNorm(s)."""
