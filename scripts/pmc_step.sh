@@ -4,7 +4,8 @@
 #   f: HBM-side fetch bytes (TCC FETCH_SIZE)      w: write bytes (TCC WRITE_SIZE)
 #   l (PMC_LDS=1): LDS bank conflicts / LDS-active cycles, LDS and any-dependency waits
 # over a 2-step GPT-2 bench, then the per-kernel-group table of scripts/pmc_step_summary.py.
-# usage: [PMC_PASS_TIMEOUT=seconds] scripts/pmc_step.sh TAG [bench args]
+# usage: [PMC_PASS_TIMEOUT=seconds] [PMC_SKIP_STEPS=n] scripts/pmc_step.sh TAG [bench args]
+# (PMC_SKIP_STEPS: leave the first n optimizer steps -- the bench's warmup -- out of the table)
 set -o pipefail
 cd "$(dirname "$0")/.."
 REPO=$(pwd)
@@ -26,5 +27,5 @@ run w WRITE_SIZE GRBM_GUI_ACTIVE && \
 { [[ -z $PMC_LDS ]] || run l SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE; }
 rc=$?
 cd "$REPO" || exit 1
-python3 scripts/pmc_step_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+python3 scripts/pmc_step_summary.py "$OUT" "${PMC_SKIP_STEPS:-0}" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
 exit $rc

@@ -79,12 +79,22 @@ def load(d, p):
     return {k: (names[k], per[k], dur.get(k, 0)) for k in sorted(per)}
 
 
+def steady(ks, skip):
+    """The dispatches after the ``skip``-th optimizer kernel (warmup steps, and with them one-time
+    work such as the hipBLASLt wrapper's first-use solution sweep, csrc/blaslt.cpp)."""
+    if skip <= 0:
+        return ks
+    ends = [i for i, k in enumerate(ks) if "adamw" in k[0]]
+    return ks[ends[skip - 1] + 1:] if len(ends) >= skip else ks
+
+
 def main():
     d = sys.argv[1]
+    skip = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     m, f, w, lp = load(d, "m"), load(d, "f"), load(d, "w"), load(d, "l")
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     other = collections.defaultdict(float)
-    mk, fk, wk, lk = list(m.values()), list(f.values()), list(w.values()), list(lp.values())
+    mk, fk, wk, lk = (steady(list(x.values()), skip) for x in (m, f, w, lp))
     for i, (name, c, ns) in enumerate(mk):
         g = agg[group(name)]
         g["n"] += 1
@@ -103,7 +113,8 @@ def main():
                         "SQ_BUSY_CYCLES", "SQ_WAIT_ANY"):
                 g[key] += lc.get(key, 0.0)
     tot = sum(g["ns"] for g in agg.values())
-    print(f"{len(mk)} dispatches, {tot / 1e6:.2f} ms of kernels (2-step bench under the counter pass)")
+    what = f"after {skip} warmup step(s)" if skip else "the whole bench run"
+    print(f"{len(mk)} dispatches, {tot / 1e6:.2f} ms of kernels ({what}, under the counter passes)")
     extra = bool(lk)
     hdr = f"{'group':44s} {'ms':>8s} {'%':>5s} {'MFMA util':>9s} {'clk GHz':>7s} {'L2-EA GB':>8s} {'TB/s':>6s}"
     if extra:  # LDS bank-conflict cycles per LDS-active cycle; LDS / any waits per wave cycle

@@ -90,6 +90,17 @@ def test_pmc_step_summary_utilisation_and_traffic(tmp_path):
     assert gemm[-3:] == ["25.0%", "10.0%", "30.0%"], gemm
 
 
+def test_pmc_step_summary_skips_warmup_steps():
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import pmc_step_summary as pss
+    ks = [("tune", {}, 1), ("adamw_flat_kernel", {}, 1), ("gemm", {}, 2), ("adamw_flat_kernel", {}, 1),
+          ("gemm", {}, 3), ("adamw_flat_kernel", {}, 1)]
+    assert pss.steady(ks, 0) == ks
+    assert pss.steady(ks, 1) == ks[2:]
+    assert pss.steady(ks, 2) == ks[4:]
+    assert pss.steady(ks, 9) == ks  # fewer steps than asked: keep everything
+
+
 def test_pmc_step_summary_groups_gemm16_by_epilogue():
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import pmc_step_summary as pss
