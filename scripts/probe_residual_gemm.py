@@ -65,4 +65,9 @@ for name, N, K in (("qkv+bias", 2304, 768), ("attn_proj", 768, 768), ("fc2", 768
            / torch.nn.functional.linear(h, w, b).float().norm()).item()
     print(json.dumps({"plain": name, "linear_bias_ms": round(t_lin, 4), "wrapper_ms": round(t_own, 4),
                       "rel_diff": f"{err:.2e}"}))
+# residual without the bias (beta = 1, no bias epilogue): the solutions that support it
+for name, K in (("attn_proj", 768), ("fc2", 3072)):
+    h, w = mk(M, K), mk(D, K)
+    t_nb = med(lambda: C().linear_residual(h, w, None, x))
+    print(json.dumps({"residual_no_bias": name, "ms": round(t_nb, 4)}))
 
